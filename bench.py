@@ -1,0 +1,468 @@
+#!/usr/bin/env python3
+"""bench.py -- HiCCL bucket-reduction stage on MI355X (driver contract).
+
+Default workload = BASELINE config 2: N = 8 inputs x 2^28 fp32 (1 GiB each)
+-> one 1 GiB output, device-resident.  One "step" = one hiccl_reduce launch
+over the whole bucket.  value = whole-job GB/s = world_size x (N+1) x count x
+4 B x steps / max-over-ranks wall time (the reference's own byte accounting,
+source/compute.h:251-257).  Multi-GPU: every rank reduces its own bucket
+(replicas, weak scaling -- the stage is per-GPU local).
+
+Extra objects on the JSON line:
+  roofline      achieved = algorithmic bytes per launch / mean kernel time from
+                HIP events on the launch stream; peak = 8000 GB/s (MI355X HBM3E
+                spec); traffic = PMC HBM bytes per launch from the committed
+                profiles/ PMC summary when one matches this workload, else null.
+  cpu_baseline  the reference's own CPU reduce_kernel (compute.h:14-23, built
+                from /root/reference into oracle/_ref by oracle/build_ref.sh;
+                kind "reference") or the C restatement (kind "port"), timed on
+                this host, rank 0 at N=1 only.
+
+Other modes (not the driver's line): --sweep (tuning variants, interleaved in
+one process), --nway (config 3), --chunks (config 4), --roundtrip (host
+memory H2D + kernel + D2H rate for DESIGN.md).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import hiccl_amd  # noqa: E402
+from hiccl_amd import _lib as L  # noqa: E402
+
+METRIC = "GB/s device-resident N-way float bucket sum, 1 GB/input; % HBM peak"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+SEED = 1234
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ----------------------------------------------------------------- dist ----
+
+class Dist:
+    def __init__(self, gpus):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != gpus:
+            if self.world == 1:
+                log(f"bench: --gpus {gpus} without a launcher; running 1 rank")
+                self.world = 1
+            else:
+                log(f"bench: WORLD_SIZE={self.world} but --gpus {gpus}")
+        torch.cuda.set_device(self.local)
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            self.pg = dist
+
+    def barrier(self):
+        if self.pg:
+            self.pg.barrier(device_ids=[self.local])
+
+    def max(self, x):
+        if not self.pg:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.pg:
+            self.pg.destroy_process_group()
+
+
+# ----------------------------------------------------------- workloads -----
+
+def make_bucket(n, count, dtype=torch.float32, seed=SEED):
+    ins = [torch.empty(count, dtype=dtype, device="cuda") for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, seed, k)
+    out = torch.empty(count, dtype=dtype, device="cuda")
+    torch.cuda.synchronize()
+    return ins, out
+
+
+def time_launches(fn, steps, warmup, dist=None):
+    """W untimed launches, then K timed: barrier + sync on both sides.
+    Returns (wall seconds for K steps, list of per-launch kernel ms)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(s)
+        fn()
+        b.record(s)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    return t1 - t0, [a.elapsed_time(b) for a, b in evs]
+
+
+def copy_ceiling(nbytes=1 << 30, reps=10):
+    src = torch.empty(nbytes // 4, device="cuda")
+    dst = torch.empty_like(src)
+    hiccl_amd.fill_uniform(src, 1, 0)
+    _, ms = time_launches(lambda: hiccl_amd.stream_copy(dst, src), reps, 3)
+    del src, dst
+    return 2 * nbytes / (np.mean(ms) * 1e-3) / 1e9
+
+
+# --------------------------------------------------------- CPU baseline ----
+
+def cpu_baseline(n, count, budget_s=10.0):
+    """The reference's CPU reduce_kernel (or the restatement) on this host.
+
+    Sample: the full config-2 bucket (n x count fp32), first-touch-initialised
+    in parallel by the oracle generator, reduced repeatedly until ~budget_s
+    of CPU work; reports the median pass."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libhiccl_ref.so")
+    ora_so = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not os.path.exists(ora_so):
+        return None
+    ora = ctypes.CDLL(ora_so)
+    ora.oracle_num_threads.restype = ctypes.c_int
+    threads = ora.oracle_num_threads()
+    if os.path.exists(ref_so):
+        lib, kind = ctypes.CDLL(ref_so), "reference"
+        fn = lib.ref_reduce_f32
+        fn.restype = None
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int]
+    else:
+        lib, kind = ora, "port"
+        fn = ora.oracle_reduce_f32
+        fn.restype = None
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+    fill = ora.oracle_fill_uniform_f32
+    fill.restype = None
+    fill.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t]
+    bufs = [np.empty(count, np.float32) for _ in range(n)]
+    for k, b in enumerate(bufs):
+        fill(b.ctypes.data, count, SEED, k, 0)
+    out = np.empty(count, np.float32)
+    fill(out.ctypes.data, count, SEED, 99, 0)  # first touch of the output
+    tab = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+
+    def one():
+        t = time.perf_counter()
+        if kind == "reference":
+            fn(out.ctypes.data, count, tab, n)
+        else:
+            fn(out.ctypes.data, tab, n, count)
+        return time.perf_counter() - t
+
+    one()  # warm
+    times = []
+    t_start = time.perf_counter()
+    while time.perf_counter() - t_start < budget_s and len(times) < 50:
+        times.append(one())
+    med = float(np.median(times))
+    # spot-check the CPU result against the generator at a few indices
+    idx = np.array([0, 1, count // 2, count - 1], np.uint64)
+    chk = np.empty(4, np.float32)
+    ss = ora.oracle_sample_sum_f32
+    ss.restype = None
+    ss.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int]
+    ss(chk.ctypes.data, idx.ctypes.data, 4, SEED, n)
+    assert np.array_equal(chk.view(np.uint32), out[idx.astype(np.int64)].view(np.uint32))
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    gbps = (n + 1) * count * 4 / med / 1e9
+    del bufs, out
+    return {"value": round(gbps, 2), "unit": "GB/s", "cores": threads, "kind": kind,
+            "sample": f"{n} x 2^{int(np.log2(count))} fp32 -> 1 output (the full config-2 bucket), "
+                      f"median of {len(times)} passes ({med * 1e3:.1f} ms each), "
+                      f"OpenMP {threads} threads, {cpu_model}"}
+
+
+def traffic_from_profiles(n, count):
+    """HBM bytes per launch from a committed PMC summary for this workload."""
+    pdir = os.path.join(ROOT, "profiles")
+    best = None
+    if not os.path.isdir(pdir):
+        return None
+    for f in sorted(os.listdir(pdir)):
+        if f.endswith("_pmc.json"):
+            try:
+                d = json.load(open(os.path.join(pdir, f)))
+            except (OSError, ValueError):
+                continue
+            if d.get("n_inputs") == n and d.get("count") == count and d.get("hbm_bytes_per_launch"):
+                best = d
+    return best
+
+
+# ------------------------------------------------------------------ main ----
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=8, help="inputs per bucket")
+    ap.add_argument("--log2count", type=int, default=28, help="elements per input = 2^x")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--block", type=int, default=0)
+    ap.add_argument("--unroll", type=int, default=0)
+    ap.add_argument("--bpc", type=int, default=0)
+    ap.add_argument("--nt", type=int, default=0)
+    ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--nway", action="store_true")
+    ap.add_argument("--chunks", action="store_true")
+    ap.add_argument("--roundtrip", action="store_true")
+    args = ap.parse_args()
+
+    dist = Dist(args.gpus)
+    if args.sweep:
+        return sweep(args)
+    if args.nway:
+        return nway(args)
+    if args.chunks:
+        return chunks(args)
+    if args.roundtrip:
+        return roundtrip(args)
+
+    n, count = args.n, 1 << args.log2count
+    cfg = None
+    if args.block or args.unroll or args.bpc or args.nt:
+        cfg = dict(block=args.block, unroll=args.unroll, blocks_per_cu=args.bpc, nontemporal=args.nt)
+    ins, out = make_bucket(n, count)
+    step = lambda: hiccl_amd.reduce(out, ins, config=cfg)  # noqa: E731
+    wall, kms = time_launches(step, args.steps, args.warmup, dist)
+    wall_max = dist.max(wall)
+    bytes_step = (n + 1) * count * 4
+    value = dist.world * bytes_step * args.steps / wall_max / 1e9
+    kern_s = float(np.mean(kms)) * 1e-3
+    achieved = bytes_step / kern_s / 1e9
+
+    # parity spot check of this very output against the oracle generator
+    parity = None
+    ora_so = os.path.join(ROOT, "oracle", "liboracle.so")
+    if os.path.exists(ora_so):
+        ora = ctypes.CDLL(ora_so)
+        idx = np.random.default_rng(dist.rank).integers(0, count, 1024).astype(np.uint64)
+        exp = np.empty(len(idx), np.float32)
+        ora.oracle_sample_sum_f32.restype = None
+        ora.oracle_sample_sum_f32(ctypes.c_void_p(exp.ctypes.data), ctypes.c_void_p(idx.ctypes.data),
+                                  ctypes.c_size_t(len(idx)), ctypes.c_uint64(SEED), ctypes.c_int(n))
+        got = out[torch.from_numpy(idx.astype(np.int64)).cuda()].cpu().numpy()
+        parity = bool(np.array_equal(got.view(np.uint32), exp.view(np.uint32)))
+        if not parity:
+            log("bench: PARITY FAILURE against the oracle sample")
+    del ins, out
+    torch.cuda.empty_cache()
+
+    copy_gbps = copy_ceiling() if dist.rank == 0 else None
+    prof = traffic_from_profiles(n, count)
+    cpu = None
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(n, count, args.cpu_budget)
+    dist.close()
+    if dist.rank != 0:
+        return 0
+    props = torch.cuda.get_device_properties(0)
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": dist.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (uniform [-1,1) counter-hash, device-generated)",
+        "config": {"workload": f"C2: {n} inputs x 2^{args.log2count} fp32 ({count * 4 >> 20} MiB/input) -> 1 output, "
+                               "device-resident, one hiccl_reduce launch per step",
+                   "n_inputs": n, "count": count, "bytes_per_step": bytes_step,
+                   "kernel_config": cfg or "default", "parallelism": f"replicas x{dist.world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": (prof or {}).get("hbm_bytes_per_launch"),
+                     "kernel_ms_mean": round(kern_s * 1e3, 4), "kernel_ms_min": round(min(kms), 4),
+                     "copy_ceiling_GBps": round(copy_gbps, 1) if copy_gbps else None,
+                     "frac_of_copy": round(achieved / copy_gbps, 4) if copy_gbps else None,
+                     "traffic_source": (prof or {}).get("source")},
+        "cpu_baseline": cpu,
+        "parity_sample_ok": parity,
+        "device": props.name,
+    }
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+def sweep(args):
+    """Interleaved A/B of kernel variants in one process (rule 24)."""
+    n, count = args.n, 1 << args.log2count
+    ins, out = make_bucket(n, count)
+    variants = []
+    for block in (256, 512):
+        for unroll in (1, 2, 4):
+            for nt in (0, 1, 2):
+                for bpc in (0, 2, 4, 8):
+                    variants.append(dict(block=block, unroll=unroll, nontemporal=nt, blocks_per_cu=bpc))
+    res = {i: [] for i in range(len(variants))}
+    for rnd in range(3):
+        for i, v in enumerate(variants):
+            try:
+                _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins, config=v), 5, 2)
+            except Exception as e:  # unsupported combination
+                log("skip", v, e)
+                continue
+            res[i].append(float(np.median(ms)))
+        log(f"sweep round {rnd} done")
+    bytes_step = (n + 1) * count * 4
+    rows = []
+    for i, v in enumerate(variants):
+        if res[i]:
+            t = float(np.median(res[i]))
+            rows.append((bytes_step / t / 1e6, t, v))
+    rows.sort(key=lambda r: -r[0])
+    for gbps, t, v in rows:
+        print(json.dumps({"GBps": round(gbps, 1), "ms": round(t, 4), "frac": round(gbps / HBM_PEAK_GBPS, 4), **v}))
+    return 0
+
+
+def nway(args):
+    """Config 3: N in 2..64 inputs x 2^26 fp32 (256 MiB each)."""
+    count = 1 << 26
+    copy_gbps = copy_ceiling()
+    for n in (2, 3, 4, 8, 16, 32, 64):
+        ins, out = make_bucket(n, count)
+        _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins), args.steps, args.warmup)
+        t = float(np.median(ms)) * 1e-3
+        b = (n + 1) * count * 4
+        print(json.dumps({"config": "C3", "n": n, "count": count, "kernel_ms": round(t * 1e3, 4),
+                          "GBps": round(b / t / 1e9, 1), "frac_hbm": round(b / t / 1e9 / HBM_PEAK_GBPS, 4),
+                          "read_GBps": round(n * count * 4 / t / 1e9, 1),
+                          "frac_of_copy": round(b / t / 1e9 / copy_gbps, 4)}), flush=True)
+        del ins, out
+        torch.cuda.empty_cache()
+    return 0
+
+
+def chunks(args):
+    """Config 4: fp32/bf16, 16 MiB..4 GiB per input, split into 1 MiB computes
+    (pipedepth = bytes / 1 MiB, reduce.h:406 split), batched plan launch vs
+    one launch per compute (the reference structure, compute.h:141-145)."""
+    n = 8
+    for dtype in (torch.float32, torch.bfloat16):
+        esz = torch.tensor([], dtype=dtype).element_size()
+        for mib in (16, 64, 256, 1024, 4096):
+            count = (mib << 20) // esz
+            free, _ = torch.cuda.mem_get_info()
+            if (n + 1) * count * esz * 1.05 > free:
+                log(f"chunks: skip {mib} MiB ({dtype}): not enough memory")
+                continue
+            ins, out = make_bucket(n, count, dtype)
+            depth = max(1, (mib << 20) // (1 << 20))
+            comp = hiccl_amd.Compute(dtype, device=torch.cuda.current_device())
+            off = 0
+            for b in range(depth):  # partition(): count/numbatch + (b < count%numbatch)
+                c = count // depth + (1 if b < count % depth else 0)
+                comp.add([(t, off) for t in ins], (out, off), c, compid=0)
+                off += c
+            stream = torch.cuda.current_stream()
+            res = {}
+            for mode in ("batched", "each"):
+                _, ms = time_launches(lambda: comp.start(stream=stream, each=(mode == "each")),
+                                      args.steps, args.warmup)
+                t = float(np.median(ms)) * 1e-3
+                res[mode] = t
+            b = (n + 1) * count * esz
+            print(json.dumps({"config": "C4", "dtype": str(dtype).split(".")[-1], "mib_per_input": mib,
+                              "computes": depth, "batched_ms": round(res["batched"] * 1e3, 4),
+                              "batched_GBps": round(b / res["batched"] / 1e9, 1),
+                              "each_ms": round(res["each"] * 1e3, 4),
+                              "each_GBps": round(b / res["each"] / 1e9, 1)}), flush=True)
+            comp.close()
+            del ins, out
+            torch.cuda.empty_cache()
+    return 0
+
+
+def roundtrip(args):
+    """Inputs and output in pinned host memory: H2D of N inputs + kernel + D2H
+    (serial, and chunk-pipelined over 3 streams)."""
+    n, count = args.n, 1 << args.log2count
+    host_in = [torch.empty(count, dtype=torch.float32).pin_memory() for _ in range(n)]
+    for k, h in enumerate(host_in):
+        h.copy_(torch.from_numpy(np.random.default_rng(k).uniform(-1, 1, count).astype(np.float32)))
+    host_out = torch.empty(count, dtype=torch.float32).pin_memory()
+    dev_in = [torch.empty(count, device="cuda") for _ in range(n)]
+    dev_out = torch.empty(count, device="cuda")
+
+    def serial():
+        for h, d in zip(host_in, dev_in):
+            d.copy_(h, non_blocking=True)
+        hiccl_amd.reduce(dev_out, dev_in)
+        host_out.copy_(dev_out, non_blocking=True)
+
+    nchunk = 16
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    csz = count // nchunk
+
+    def pipelined():
+        cur = torch.cuda.current_stream()
+        for s in streams:
+            s.wait_stream(cur)
+        for c in range(nchunk):
+            s = streams[c % 3]
+            lo = c * csz
+            hi = count if c == nchunk - 1 else lo + csz
+            with torch.cuda.stream(s):
+                for h, d in zip(host_in, dev_in):
+                    d[lo:hi].copy_(h[lo:hi], non_blocking=True)
+                hiccl_amd.reduce(dev_out[lo:], [d[lo:] for d in dev_in], count=hi - lo, stream=s)
+                host_out[lo:hi].copy_(dev_out[lo:hi], non_blocking=True)
+        for s in streams:
+            cur.wait_stream(s)
+
+    out = {}
+    for name, fn in (("serial", serial), ("pipelined", pipelined)):
+        wall, _ = time_launches(fn, 5, 2)
+        t = wall / 5
+        out[name] = {"s": round(t, 4), "GBps_alg": round((n + 1) * count * 4 / t / 1e9, 2)}
+    # device-only reference
+    _, ms = time_launches(lambda: hiccl_amd.reduce(dev_out, dev_in), 10, 3)
+    out["kernel_only_GBps"] = round((n + 1) * count * 4 / (np.median(ms) * 1e-3) / 1e9, 1)
+    exp = host_in[0].clone()
+    for h in host_in[1:]:
+        exp = exp + h
+    torch.cuda.synchronize()
+    out["parity_ok"] = bool(torch.equal(exp.view(torch.int32), host_out.view(torch.int32)))
+    print(json.dumps({"mode": "roundtrip", "n": n, "count": count, **out,
+                      "pcie_bytes": (n + 1) * count * 4}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

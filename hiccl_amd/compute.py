@@ -1,0 +1,215 @@
+"""Python mirror of the reference's reduction compute stage.
+
+``reduce`` is one registered compute launched once (source/compute.h:145);
+``Compute`` mirrors ``HiCCL::Compute<T>`` (source/compute.h:80-258):
+``add`` / ``start`` / ``wait`` / ``report`` / ``measure`` with the same
+argument meaning.  Both call straight into the HIP library through the C ABI
+(include/hiccl_reduce.h); device memory and streams come from torch.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+
+def _stream_handle(stream):
+    if stream is None:
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _ptr_table(ptrs):
+    t = (ctypes.c_void_p * max(1, len(ptrs)))()
+    for k, p in enumerate(ptrs):
+        t[k] = p
+    return t
+
+
+def _dtype_code(t):
+    try:
+        return L.DTYPE_OF_TORCH[t.dtype]
+    except KeyError:
+        raise TypeError(f"hiccl: unsupported dtype {t.dtype}") from None
+
+
+def _check_tensor(t, what):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"hiccl: {what} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise ValueError(f"hiccl: {what} must be a device tensor (the HIP path has no CPU mode)")
+    if not t.is_contiguous():
+        raise ValueError(f"hiccl: {what} must be contiguous")
+
+
+def reduce(out, inputs, count=None, stream=None, config=None):
+    """out[:count] = ((0 + inputs[0]) + inputs[1]) + ... in the list order.
+
+    Mirrors one compute of compute.h: inputs are summed in list order with
+    the accumulator starting at 0 in the element type.  ``out`` may be one
+    of the inputs (in place).  Asynchronous on ``stream`` (default: torch's
+    current stream).  ``config``: dict of hiccl_reduce_config_t fields.
+    """
+    _check_tensor(out, "out")
+    if count is None:
+        count = out.numel()
+    dt = _dtype_code(out)
+    ptrs = []
+    for k, x in enumerate(inputs):
+        _check_tensor(x, f"inputs[{k}]")
+        if x.dtype != out.dtype:
+            raise TypeError(f"hiccl: inputs[{k}] dtype {x.dtype} != out dtype {out.dtype}")
+        if x.numel() < count:
+            raise ValueError(f"hiccl: inputs[{k}] has {x.numel()} < count={count} elements")
+        ptrs.append(x.data_ptr())
+    if out.numel() < count:
+        raise ValueError(f"hiccl: out has {out.numel()} < count={count} elements")
+    tab = _ptr_table(ptrs)
+    s = _stream_handle(stream)
+    if config is None:
+        rc = L.lib().hiccl_reduce(dt, ctypes.c_void_p(out.data_ptr()), tab, len(ptrs), count, s)
+    else:
+        cfg = L.ReduceConfig(**config)
+        rc = L.lib().hiccl_reduce_ex(dt, ctypes.c_void_p(out.data_ptr()), tab, len(ptrs), count, s,
+                                     ctypes.byref(cfg))
+    L.check(rc, "hiccl_reduce")
+    return out
+
+
+def reduce_ptrs(dtype_code, out_ptr, in_ptrs, count, stream=None, config=None):
+    """Raw-pointer form (pointers already offset), used by the Comm layer."""
+    tab = _ptr_table(list(in_ptrs))
+    s = _stream_handle(stream)
+    if config is None:
+        rc = L.lib().hiccl_reduce(dtype_code, ctypes.c_void_p(out_ptr), tab, len(in_ptrs), count, s)
+    else:
+        cfg = L.ReduceConfig(**config)
+        rc = L.lib().hiccl_reduce_ex(dtype_code, ctypes.c_void_p(out_ptr), tab, len(in_ptrs), count, s,
+                                     ctypes.byref(cfg))
+    L.check(rc, "hiccl_reduce")
+
+
+class Compute:
+    """``HiCCL::Compute<T>`` (source/compute.h:80-258) on the batched plan.
+
+    add(inputbuf, outputbuf, count, compid)  compute.h:101-139 -- records the
+        compute only when ``myid == compid`` (SPMD: every rank calls add).
+        ``inputbuf`` is a list of tensors or (tensor, element_offset) pairs,
+        ``outputbuf`` a tensor or (tensor, element_offset).
+    start()   compute.h:141-160 -- ONE batched kernel for all computes.
+    wait()    compute.h:161-171.
+    report()  compute.h:173-189 (local numbers; the Comm layer gathers).
+    measure(warmup, numiter[, count])  compute.h:191-257.
+    """
+
+    def __init__(self, dtype=torch.float32, device=None, myid=0, acc=L.HICCL_ACC_NATIVE):
+        self.dtype = dtype
+        self.code = L.DTYPE_OF_TORCH[dtype]
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = device
+        self.myid = myid
+        self.numcomp = 0
+        self.inputbuf = []
+        self.outputbuf = []
+        self.count = []
+        self._keep = []  # keep tensors alive while registered
+        h = ctypes.c_void_p()
+        L.check(L.lib().hiccl_reduce_plan_create(ctypes.byref(h), self.code, device), "plan_create")
+        self._plan = h
+        if acc != L.HICCL_ACC_NATIVE:
+            L.check(L.lib().hiccl_reduce_plan_set_acc(self._plan, acc), "plan_set_acc")
+
+    @staticmethod
+    def _ptr(buf, esz):
+        if isinstance(buf, tuple):
+            t, off = buf
+        else:
+            t, off = buf, 0
+        return t, t.data_ptr() + off * esz
+
+    def add(self, inputbuf, outputbuf, count, compid):
+        if self.myid != compid:
+            return
+        esz = L.lib().hiccl_dtype_size(self.code)
+        ins = [self._ptr(b, esz) for b in inputbuf]
+        ot, op = self._ptr(outputbuf, esz)
+        tab = _ptr_table([p for _, p in ins])
+        L.check(L.lib().hiccl_reduce_plan_add(self._plan, ctypes.c_void_p(op), tab, len(ins), count),
+                "plan_add")
+        self._keep.append((ot, [t for t, _ in ins]))
+        self.inputbuf.append([p for _, p in ins])
+        self.outputbuf.append(op)
+        self.count.append(count)
+        self.numcomp += 1
+
+    def start(self, stream=None, each=False):
+        s = _stream_handle(stream) if stream is not None else ctypes.c_void_p(0)
+        fn = L.lib().hiccl_reduce_plan_launch_each if each else L.lib().hiccl_reduce_plan_launch
+        L.check(fn(self._plan, s), "plan_launch")
+
+    def wait(self):
+        L.check(L.lib().hiccl_reduce_plan_sync(self._plan), "plan_sync")
+
+    def bytes(self):
+        """Sum of count * (n + 1) * sizeof(T) (compute.h:251-257)."""
+        return L.lib().hiccl_reduce_plan_bytes(self._plan)
+
+    def report(self):
+        numinput = sum(len(x) for x in self.inputbuf)
+        return f"numcomp: {self.numcomp}({numinput})"
+
+    def measure(self, warmup, numiter, count=None, each=False):
+        """Time start()+wait() like compute.h:191-250; returns the stats dict.
+
+        ``count`` is the element count the GB/s figure is priced on
+        (compute.h:242); default = the two-argument overload's
+        sum of count*(n+1) (compute.h:251-257), i.e. reads + writes.
+        """
+        import time
+        data = (self.bytes() if count is None else count * torch.tensor([], dtype=self.dtype).element_size())
+        times = []
+        for it in range(-warmup, numiter):
+            torch.cuda.synchronize(self.device)
+            t0 = time.perf_counter()
+            self.start(each=each)
+            self.wait()
+            t = time.perf_counter() - t0
+            if it >= 0:
+                times.append(t)
+        times.sort()
+        avg = sum(times) / len(times)
+        stats = {"min": times[0], "median": times[len(times) // 2], "max": times[-1], "avg": avg,
+                 "data": data}
+        for k in ("min", "median", "max", "avg"):
+            stats[k + "_GBps"] = data / stats[k] / 1e9
+        return stats
+
+    def close(self):
+        if self._plan:
+            L.lib().hiccl_reduce_plan_destroy(self._plan)
+            self._plan = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def fill_uniform(t, seed, k, first=0, stream=None):
+    """Synthetic input k: uniform [-1,1) of hash(seed, k, first + i) (matches the oracle)."""
+    _check_tensor(t, "t")
+    L.check(L.lib().hiccl_fill_uniform(_dtype_code(t), ctypes.c_void_p(t.data_ptr()), t.numel(),
+                                       seed, k, first, _stream_handle(stream)), "fill_uniform")
+    return t
+
+
+def stream_copy(dst, src, nbytes=None, stream=None):
+    """Plain 16-B/lane device copy (the achievable-bandwidth ceiling)."""
+    if nbytes is None:
+        nbytes = src.numel() * src.element_size()
+    L.check(L.lib().hiccl_stream_copy(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src.data_ptr()),
+                                      nbytes, _stream_handle(stream)), "stream_copy")

@@ -1,0 +1,959 @@
+// hiccl_amd/csrc/reduce.hip -- MI355X (gfx950 / CDNA4) bucket-reduction stage.
+//
+// Implements include/hiccl_reduce.h.  The arithmetic is the reference's
+// reduce_kernel<T> (source/compute.h:2-12 GPU, :14-23 CPU):
+//
+//     T acc = 0; for (k = 0; k < n; k++) acc += in[k][i]; out[i] = acc;
+//
+// reproduced bit for bit (same order, accumulator starts at +0 in T, every
+// add rounded to T, no FMA, no tree).  Everything else is MI355X-first:
+//
+//  * pure HBM stream, (n + 1) * sizeof(T) bytes per element, no MFMA;
+//  * 16-byte packets per lane (global_load_dwordx4 with an SGPR base +
+//    32-bit lane offset), U packets per input per lane per tile, so each
+//    lane has G*U independent 16-B loads in flight before the in-order adds;
+//  * a persistent grid (CUs x blocks_per_cu workgroups) sweeping tiles
+//    grid-stride, full tiles unpredicated;
+//  * the input pointer table travels in the kernarg segment (scalar loads,
+//    no device-side T** table and no H2D copy per call, cf. compute.h:124-126);
+//  * the output is 16-B aligned by peeling a scalar head; inputs may be
+//    mutually misaligned (partition() element offsets, reduce.h:401-415):
+//    gfx950 serves unaligned dwordx4 loads in hardware;
+//  * a batched plan kernel runs every compute of a pipeline step in ONE launch
+//    from a device descriptor table (vs one kernel + one stream + one
+//    hipStreamSynchronize per compute, compute.h:141-171).
+//
+// Layout / roofline / measured numbers: DESIGN.md.
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hiccl_reduce.h"
+
+#define HICCL_VERSION_INT 100  // 0.1.0
+
+namespace {
+
+// ------------------------------------------------------------------ errors --
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int check_hip(hipError_t e, const char *what) {
+  if (e != hipSuccess) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return (int)e;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------ vector types --
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte packet type with 1-byte alignment: a misaligned input still loads
+// as one global_load_dwordx4 (gfx950 unaligned access mode).
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kPacket = 16;  // bytes per lane per load
+
+// Buffer resources: one SGPR descriptor per input per tile (base = input +
+// tile offset, range = the tile's valid bytes).  Loads/stores then take only
+// the tile-invariant 32-bit lane offset, and the hardware range check turns
+// the lanes past the end of the last (partial) tile into no-ops.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kRsrcFlags = 0x00020000;  // raw buffer, 32-bit data format
+
+__device__ __forceinline__ rsrc_t make_rsrc(const char *base, uint32_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nbytes, kRsrcFlags);
+}
+
+// Cache policy: NT >= 1 marks loads nontemporal (aux bit 1 = nt), NT >= 2
+// marks stores nontemporal too.
+template <int NT>
+__device__ __forceinline__ u32x4 load_pkt(rsrc_t r, uint32_t voff) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, NT >= 1 ? 2 : 0);
+}
+
+template <int NT>
+__device__ __forceinline__ void store_pkt(rsrc_t r, uint32_t voff, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, 0, NT >= 2 ? 2 : 0);
+}
+
+// bf16 <-> f32.  f32 -> bf16 is round-to-nearest-even; on gfx950 the cast
+// lowers to v_cvt_pk_bf16_f32, which keeps a NaN a NaN.
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ uint32_t bf_pack(float lo, float hi) {
+  bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ uint16_t bf_round(float f) {
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
+}
+
+// ------------------------------------------------------------ element ops --
+// Each op: elem size, packet accumulator (acc_t) with zero/add/pack, and a
+// scalar accumulator for the peeled head/tail elements.  zero() + x keeps the
+// reference's `T acc = 0; acc += x` (so -0 inputs sum to +0).
+
+struct OpF32 {
+  static constexpr int kEsz = 4;
+  typedef f32x4 acc_t;
+  __device__ static acc_t zero() { return (f32x4)(0.0f); }
+  __device__ static acc_t add(acc_t a, u32x4 p) { return a + __builtin_bit_cast(f32x4, p); }
+  __device__ static u32x4 pack(acc_t a) { return __builtin_bit_cast(u32x4, a); }
+  typedef float sacc_t;
+  __device__ static sacc_t szero() { return 0.0f; }
+  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + *(const float *)p; }
+  __device__ static void sstore(char *p, sacc_t a) { *(float *)p = a; }
+};
+
+struct OpF64 {
+  static constexpr int kEsz = 8;
+  typedef f64x2 acc_t;
+  __device__ static acc_t zero() { return (f64x2)(0.0); }
+  __device__ static acc_t add(acc_t a, u32x4 p) { return a + __builtin_bit_cast(f64x2, p); }
+  __device__ static u32x4 pack(acc_t a) { return __builtin_bit_cast(u32x4, a); }
+  typedef double sacc_t;
+  __device__ static sacc_t szero() { return 0.0; }
+  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + *(const double *)p; }
+  __device__ static void sstore(char *p, sacc_t a) { *(double *)p = a; }
+};
+
+struct OpU64 {
+  static constexpr int kEsz = 8;
+  typedef u64x2 acc_t;
+  __device__ static acc_t zero() { return (u64x2)(0); }
+  __device__ static acc_t add(acc_t a, u32x4 p) { return a + __builtin_bit_cast(u64x2, p); }
+  __device__ static u32x4 pack(acc_t a) { return __builtin_bit_cast(u32x4, a); }
+  typedef uint64_t sacc_t;
+  __device__ static sacc_t szero() { return 0; }
+  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + *(const uint64_t *)p; }
+  __device__ static void sstore(char *p, sacc_t a) { *(uint64_t *)p = a; }
+};
+
+struct OpI32 {  // two's-complement wrap-around, done in unsigned
+  static constexpr int kEsz = 4;
+  typedef u32x4 acc_t;
+  __device__ static acc_t zero() { return (u32x4)(0u); }
+  __device__ static acc_t add(acc_t a, u32x4 p) { return a + p; }
+  __device__ static u32x4 pack(acc_t a) { return a; }
+  typedef uint32_t sacc_t;
+  __device__ static sacc_t szero() { return 0u; }
+  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + *(const uint32_t *)p; }
+  __device__ static void sstore(char *p, sacc_t a) { *(uint32_t *)p = a; }
+};
+
+// bf16, reference semantics: acc is bf16, every add = f32 add then round to
+// bf16.  The accumulator is kept as f32 values that are exact bf16 numbers.
+struct OpBF16 {
+  static constexpr int kEsz = 2;
+  typedef f32x8 acc_t;
+  __device__ static acc_t zero() { return (f32x8)(0.0f); }
+  __device__ static acc_t add(acc_t a, u32x4 p) {
+    acc_t r;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      float s0 = a[2 * w] + bf_lo(p[w]);
+      float s1 = a[2 * w + 1] + bf_hi(p[w]);
+      uint32_t q = bf_pack(s0, s1);
+      r[2 * w] = bf_lo(q);
+      r[2 * w + 1] = bf_hi(q);
+    }
+    return r;
+  }
+  __device__ static u32x4 pack(acc_t a) {
+    u32x4 r;
+#pragma unroll
+    for (int w = 0; w < 4; w++) r[w] = bf_pack(a[2 * w], a[2 * w + 1]);
+    return r;
+  }
+  typedef float sacc_t;
+  __device__ static sacc_t szero() { return 0.0f; }
+  __device__ static sacc_t sadd(sacc_t a, const char *p) {
+    float s = a + __uint_as_float((uint32_t)(*(const uint16_t *)p) << 16);
+    return __uint_as_float((uint32_t)bf_round(s) << 16);
+  }
+  __device__ static void sstore(char *p, sacc_t a) { *(uint16_t *)p = bf_round(a); }
+};
+
+// bf16 inputs, f32 accumulator, one rounding at the end (HICCL_ACC_WIDE).
+struct OpBF16Wide {
+  static constexpr int kEsz = 2;
+  typedef f32x8 acc_t;
+  __device__ static acc_t zero() { return (f32x8)(0.0f); }
+  __device__ static acc_t add(acc_t a, u32x4 p) {
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      a[2 * w] += bf_lo(p[w]);
+      a[2 * w + 1] += bf_hi(p[w]);
+    }
+    return a;
+  }
+  __device__ static u32x4 pack(acc_t a) {
+    u32x4 r;
+#pragma unroll
+    for (int w = 0; w < 4; w++) r[w] = bf_pack(a[2 * w], a[2 * w + 1]);
+    return r;
+  }
+  typedef float sacc_t;
+  __device__ static sacc_t szero() { return 0.0f; }
+  __device__ static sacc_t sadd(sacc_t a, const char *p) {
+    return a + __uint_as_float((uint32_t)(*(const uint16_t *)p) << 16);
+  }
+  __device__ static void sstore(char *p, sacc_t a) { *(uint16_t *)p = bf_round(a); }
+};
+
+// ----------------------------------------------------------- tile engine --
+//
+// A compute is split as [head scalars | npkt 16-B packets | tail scalars],
+// the packets 16-B aligned on the OUTPUT.  A tile = BLOCK*U packets; lane t
+// of the workgroup owns packets u*BLOCK + t (u < U), so every load
+// instruction of a wave covers 1 KiB contiguous bytes of one input.
+
+constexpr int kMaxArgInputs = 64;  // kernarg pointer table (512 B)
+
+struct SingleArgs {
+  char *out;          // raw output pointer
+  uint64_t npkt;      // body packets
+  uint64_t ntiles;    // >= 1
+  uint32_t n;         // inputs
+  uint32_t head;      // scalar elements before the body
+  uint32_t tail;      // scalar elements after the body
+  uint32_t pad;
+  const char *in[kMaxArgInputs];
+};
+
+// Descriptor of one compute in a batched plan (device memory).
+struct PlanDesc {
+  char *out;
+  const char *const *in;  // device table of n input pointers
+  uint64_t npkt;
+  uint64_t tile_begin;  // first global tile of this compute
+  uint32_t n, head, tail, pad;
+};
+static_assert(sizeof(PlanDesc) == 48, "PlanDesc layout");
+
+// Input pointer source: kernarg array or device table.
+struct ArgInputs {
+  const char *const *p;
+  __device__ const char *operator()(int k) const { return p[k]; }
+};
+
+template <class Op, class Inputs>
+__device__ __forceinline__ void scalar_part(char *out, Inputs in, uint32_t n, uint32_t head,
+                                            uint64_t npkt, uint32_t tail, int tid) {
+  constexpr int V = kPacket / Op::kEsz;
+  if (tid >= (int)(head + tail)) return;
+  uint64_t e = (tid < (int)head) ? (uint64_t)tid : (uint64_t)head + npkt * V + (tid - head);
+  uint64_t off = e * Op::kEsz;
+  typename Op::sacc_t acc = Op::szero();
+  for (uint32_t k = 0; k < n; k++) acc = Op::sadd(acc, in(k) + off);
+  Op::sstore(out + off, acc);
+}
+
+// One group of G inputs (G static): G descriptor builds (scalar), then G*U
+// independent 16-B buffer loads, then the G in-order adds per packet.
+template <class Op, int U, int G, int NT, class Inputs>
+__device__ __forceinline__ void group_at(typename Op::acc_t (&acc)[U], Inputs in, uint32_t g,
+                                         uint64_t tile_off, uint32_t tile_bytes,
+                                         const uint32_t (&voff)[U]) {
+  rsrc_t r[G];
+#pragma unroll
+  for (int j = 0; j < G; j++) r[j] = make_rsrc(in(g + j) + tile_off, tile_bytes);
+  u32x4 x[G][U];
+#pragma unroll
+  for (int j = 0; j < G; j++) {
+#pragma unroll
+    for (int u = 0; u < U; u++) x[j][u] = load_pkt<NT>(r[j], voff[u]);
+  }
+#pragma unroll
+  for (int j = 0; j < G; j++) {
+#pragma unroll
+    for (int u = 0; u < U; u++) acc[u] = Op::add(acc[u], x[j][u]);
+  }
+}
+
+// One tile: packets pkt0 + u*BLOCK + tid, tile_bytes = valid bytes of the
+// tile (< the full tile only for the last one).  Inputs are consumed as full
+// groups of 8 followed by one statically sized remainder group, so the adds
+// happen in exactly the order k = 0, 1, ..., n-1.
+template <class Op, int U, int NT, class Inputs>
+__device__ __forceinline__ void tile_body(char *outb, Inputs in, uint32_t n, uint64_t tile_off,
+                                          uint32_t tile_bytes, const uint32_t (&voff)[U]) {
+  typename Op::acc_t acc[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) acc[u] = Op::zero();
+  uint32_t g = 0;
+  for (; g + 8 <= n; g += 8) group_at<Op, U, 8, NT>(acc, in, g, tile_off, tile_bytes, voff);
+  switch (n - g) {  // wave-uniform
+    case 1: group_at<Op, U, 1, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 2: group_at<Op, U, 2, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 3: group_at<Op, U, 3, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 4: group_at<Op, U, 4, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 5: group_at<Op, U, 5, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 6: group_at<Op, U, 6, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 7: group_at<Op, U, 7, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
+    default: break;
+  }
+  rsrc_t w = make_rsrc(outb + tile_off, tile_bytes);
+#pragma unroll
+  for (int u = 0; u < U; u++) store_pkt<NT>(w, voff[u], Op::pack(acc[u]));
+}
+
+// Body inputs shifted by the head: base(k) = in[k] + head*esz.
+template <class Inner>
+struct Shifted {
+  Inner in;
+  uint64_t shift;
+  __device__ const char *operator()(int k) const { return in(k) + shift; }
+};
+
+// ------------------------------------------------------------ kernels ------
+
+template <class Op, int BLOCK, int U, int NT>
+__global__ __launch_bounds__(BLOCK) void k_reduce_single(SingleArgs a) {
+  const int tid = threadIdx.x;
+  uint32_t voff[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * BLOCK + tid) * kPacket);
+  ArgInputs raw{a.in};
+  if (blockIdx.x == 0) scalar_part<Op>(a.out, raw, a.n, a.head, a.npkt, a.tail, tid);
+  if (a.npkt == 0) return;
+  const uint64_t shift = (uint64_t)a.head * Op::kEsz;
+  Shifted<ArgInputs> in{raw, shift};
+  char *outb = a.out + shift;
+  constexpr uint64_t TILE = (uint64_t)BLOCK * U;
+  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    const uint64_t pkt0 = t * TILE;
+    const uint64_t left = a.npkt - pkt0;
+    const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
+    tile_body<Op, U, NT>(outb, in, a.n, pkt0 * kPacket, tile_bytes, voff);
+  }
+}
+
+struct TableInputs {
+  const char *const *p;
+  __device__ const char *operator()(int k) const { return p[k]; }
+};
+
+// All computes of a plan in one launch.  Global tile t belongs to compute c
+// with desc[c].tile_begin <= t < desc[c+1].tile_begin (desc[numdesc] is a
+// sentinel); c only grows along a workgroup's grid-stride walk.
+template <class Op, int BLOCK, int U, int NT>
+__global__ __launch_bounds__(BLOCK) void k_reduce_plan(const PlanDesc *__restrict__ desc,
+                                                       uint32_t c_first, uint64_t t_begin,
+                                                       uint64_t t_end) {
+  const int tid = threadIdx.x;
+  uint32_t voff[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * BLOCK + tid) * kPacket);
+  constexpr uint64_t TILE = (uint64_t)BLOCK * U;
+  uint32_t c = c_first;
+  for (uint64_t t = t_begin + blockIdx.x; t < t_end; t += gridDim.x) {
+    while (t >= desc[c + 1].tile_begin) c++;
+    const PlanDesc d = desc[c];
+    const uint64_t lt = t - d.tile_begin;
+    TableInputs raw{d.in};
+    if (lt == 0) scalar_part<Op>(d.out, raw, d.n, d.head, d.npkt, d.tail, tid);
+    const uint64_t pkt0 = lt * TILE;
+    if (pkt0 >= d.npkt) continue;
+    const uint64_t shift = (uint64_t)d.head * Op::kEsz;
+    Shifted<TableInputs> in{raw, shift};
+    const uint64_t left = d.npkt - pkt0;
+    const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
+    tile_body<Op, U, NT>(d.out + shift, in, d.n, pkt0 * kPacket, tile_bytes, voff);
+  }
+}
+
+// ------------------------------------------------------- synthetic inputs --
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float uniform_f32(uint64_t key, uint64_t i) {
+  uint64_t h = splitmix64(key + i);
+  return (float)(uint32_t)(h >> 40) * (1.0f / 8388608.0f) - 1.0f;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void k_fill(char *out, uint64_t count, uint64_t key,
+                                              uint64_t first) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < count;
+       i += (uint64_t)gridDim.x * 256) {
+    float v = uniform_f32(key, first + i);
+    if constexpr (DT == HICCL_FLOAT32) ((float *)out)[i] = v;
+    if constexpr (DT == HICCL_FLOAT64) ((double *)out)[i] = (double)v;
+    if constexpr (DT == HICCL_BFLOAT16) ((uint16_t *)out)[i] = bf_round(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_copy(u32x4 *__restrict__ dst,
+                                              const u32x4 *__restrict__ src, uint64_t npkt) {
+  constexpr int U = 4;
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t b = (uint64_t)blockIdx.x * 256 * U; b < npkt; b += stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t p = b + u * 256 + threadIdx.x;
+      if (p < npkt) v[u] = src[p];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t p = b + u * 256 + threadIdx.x;
+      if (p < npkt) dst[p] = v[u];
+    }
+  }
+}
+
+__global__ void k_copy_bytes(char *dst, const char *src, uint64_t nbytes) {
+  for (uint64_t i = threadIdx.x; i < nbytes; i += blockDim.x) dst[i] = src[i];
+}
+
+// ------------------------------------------------------------ host side ----
+
+struct DevInfo {
+  int cus = 0;
+};
+
+std::mutex g_dev_mu;
+DevInfo g_dev[64];
+
+int device_cus(int dev) {
+  if (dev < 0 || dev >= 64) return 256;
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  if (g_dev[dev].cus == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    g_dev[dev].cus = cus;
+  }
+  return g_dev[dev].cus;
+}
+
+int current_device() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) d = 0;
+  return d;
+}
+
+size_t esize(int dtype) {
+  switch (dtype) {
+    case HICCL_FLOAT32: return 4;
+    case HICCL_FLOAT64: return 8;
+    case HICCL_BFLOAT16: return 2;
+    case HICCL_UINT64: return 8;
+    case HICCL_INT32: return 4;
+    default: return 0;
+  }
+}
+
+struct Split {
+  uint32_t head, tail;
+  uint64_t npkt;
+};
+
+// [head | npkt packets | tail] with the packets 16-B aligned on `out`.
+Split split_on(const void *out, size_t count, size_t esz) {
+  const size_t V = kPacket / esz;
+  const uintptr_t mis = (uintptr_t)out % kPacket;
+  size_t head = mis ? (kPacket - mis) / esz : 0;
+  if (head > count) head = count;
+  Split s;
+  s.head = (uint32_t)head;
+  s.npkt = (count - head) / V;
+  s.tail = (uint32_t)(count - head - s.npkt * V);
+  return s;
+}
+
+// Validate pointers: element alignment, no partial overlap with the output.
+int check_buffers(void *out, const void *const *in, int n, size_t count, size_t esz) {
+  if (!out) return fail(hipErrorInvalidValue, "hiccl_reduce: out is NULL");
+  if ((uintptr_t)out % esz)
+    return fail(hipErrorInvalidValue, "hiccl_reduce: out is not element-aligned");
+  if (n < 0) return fail(hipErrorInvalidValue, "hiccl_reduce: n < 0");
+  if (n > 0 && !in) return fail(hipErrorInvalidValue, "hiccl_reduce: in is NULL");
+  const uintptr_t o0 = (uintptr_t)out, o1 = o0 + count * esz;
+  for (int k = 0; k < n; k++) {
+    const uintptr_t p = (uintptr_t)in[k];
+    if (!p) return fail(hipErrorInvalidValue, "hiccl_reduce: in[" + std::to_string(k) + "] is NULL");
+    if (p % esz)
+      return fail(hipErrorInvalidValue,
+                  "hiccl_reduce: in[" + std::to_string(k) + "] is not element-aligned");
+    const uintptr_t p1 = p + count * esz;
+    if (p != o0 && p < o1 && o0 < p1)
+      return fail(hipErrorInvalidValue, "hiccl_reduce: in[" + std::to_string(k) +
+                                            "] partially overlaps out (only exact aliasing is allowed)");
+  }
+  return 0;
+}
+
+struct Cfg {
+  int block, unroll, bpc, nt, acc;
+};
+
+Cfg resolve(const hiccl_reduce_config_t *c) {
+  Cfg r{256, 2, 8, 0, HICCL_ACC_NATIVE};
+  if (c) {
+    if (c->block) r.block = c->block;
+    if (c->unroll) r.unroll = c->unroll;
+    if (c->blocks_per_cu) r.bpc = c->blocks_per_cu;
+    r.nt = c->nontemporal;
+    r.acc = c->acc;
+  }
+  return r;
+}
+
+// ---- single-compute dispatch (template instantiation table)
+
+typedef void (*single_fn)(SingleArgs, dim3, hipStream_t);
+
+template <class Op, int B, int U, int NT>
+void launch_single_t(SingleArgs a, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((k_reduce_single<Op, B, U, NT>), grid, dim3(B), 0, s, a);
+}
+
+template <class Op, int B, int U>
+single_fn pick_nt(int nt) {
+  switch (nt) {
+    case 0: return launch_single_t<Op, B, U, 0>;
+    case 1: return launch_single_t<Op, B, U, 1>;
+    case 2: return launch_single_t<Op, B, U, 2>;
+    default: return nullptr;
+  }
+}
+
+template <class Op, int B>
+single_fn pick_u(int u, int nt) {
+  switch (u) {
+    case 1: return pick_nt<Op, B, 1>(nt);
+    case 2: return pick_nt<Op, B, 2>(nt);
+    case 4: return pick_nt<Op, B, 4>(nt);
+    default: return nullptr;
+  }
+}
+
+// Full tuning table for the headline types; default shape for the rest.
+template <class Op, bool TUNED>
+single_fn pick_single(const Cfg &c) {
+  if constexpr (TUNED) {
+    if (c.block == 256) return pick_u<Op, 256>(c.unroll, c.nt);
+    if (c.block == 512) return pick_u<Op, 512>(c.unroll, c.nt);
+    return nullptr;
+  } else {
+    if (c.block != 256 || c.unroll != 2 || c.nt != 0) return nullptr;
+    return launch_single_t<Op, 256, 2, 0>;
+  }
+}
+
+single_fn pick_single_dtype(int dtype, const Cfg &c) {
+  switch (dtype) {
+    case HICCL_FLOAT32: return pick_single<OpF32, true>(c);
+    case HICCL_BFLOAT16:
+      return c.acc == HICCL_ACC_WIDE ? pick_single<OpBF16Wide, false>(c)
+                                     : pick_single<OpBF16, true>(c);
+    case HICCL_FLOAT64: return pick_single<OpF64, false>(c);
+    case HICCL_UINT64: return pick_single<OpU64, false>(c);
+    case HICCL_INT32: return pick_single<OpI32, false>(c);
+    default: return nullptr;
+  }
+}
+
+// ---- plan dispatch (default tile shape)
+
+constexpr int kPlanBlock = 256;
+constexpr int kPlanUnroll = 2;
+constexpr uint64_t kPlanTile = (uint64_t)kPlanBlock * kPlanUnroll;
+
+typedef void (*plan_fn)(const PlanDesc *, uint32_t, uint64_t, uint64_t, dim3, hipStream_t);
+
+template <class Op>
+void launch_plan_t(const PlanDesc *d, uint32_t c0, uint64_t t0, uint64_t t1, dim3 grid,
+                   hipStream_t s) {
+  hipLaunchKernelGGL((k_reduce_plan<Op, kPlanBlock, kPlanUnroll, 0>), grid, dim3(kPlanBlock), 0, s,
+                     d, c0, t0, t1);
+}
+
+plan_fn pick_plan(int dtype, int acc) {
+  switch (dtype) {
+    case HICCL_FLOAT32: return launch_plan_t<OpF32>;
+    case HICCL_BFLOAT16: return acc == HICCL_ACC_WIDE ? launch_plan_t<OpBF16Wide> : launch_plan_t<OpBF16>;
+    case HICCL_FLOAT64: return launch_plan_t<OpF64>;
+    case HICCL_UINT64: return launch_plan_t<OpU64>;
+    case HICCL_INT32: return launch_plan_t<OpI32>;
+    default: return nullptr;
+  }
+}
+
+uint64_t tiles_for(uint64_t npkt, uint64_t tile) {
+  uint64_t t = (npkt + tile - 1) / tile;
+  return t ? t : 1;  // a compute with only scalars still owns one tile
+}
+
+// Large-n one-shot path: stage the pointer table in stream-ordered device
+// memory and run it as a one-compute plan.
+int reduce_via_table(int dtype, int acc, void *out, const void *const *in, int n, size_t count,
+                     hipStream_t s);
+
+}  // namespace
+
+// ======================================================================
+// C ABI
+// ======================================================================
+
+extern "C" {
+
+size_t hiccl_dtype_size(int dtype) { return esize(dtype); }
+
+const char *hiccl_last_error(void) { return g_last_error.c_str(); }
+
+int hiccl_version(void) { return HICCL_VERSION_INT; }
+
+int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t count,
+                    void *stream, const hiccl_reduce_config_t *cfg) {
+  const size_t esz = esize(dtype);
+  if (!esz) return fail(hipErrorInvalidValue, "hiccl_reduce: unknown dtype " + std::to_string(dtype));
+  if (count == 0) return 0;
+  if (int e = check_buffers(out, in, n, count, esz)) return e;
+  Cfg c = resolve(cfg);
+  if (c.acc != HICCL_ACC_NATIVE && c.acc != HICCL_ACC_WIDE)
+    return fail(hipErrorInvalidValue, "hiccl_reduce: bad acc mode");
+  hipStream_t s = (hipStream_t)stream;
+  if (n > kMaxArgInputs) return reduce_via_table(dtype, c.acc, out, in, n, count, s);
+
+  single_fn fn = pick_single_dtype(dtype, c);
+  if (!fn)
+    return fail(hipErrorInvalidValue, "hiccl_reduce_ex: unsupported config (block " +
+                                          std::to_string(c.block) + ", unroll " +
+                                          std::to_string(c.unroll) + ", nt " +
+                                          std::to_string(c.nt) + ") for this dtype");
+  if (c.bpc < 1 || c.bpc > 64) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: blocks_per_cu");
+
+  SingleArgs a;
+  memset(&a, 0, sizeof(a));
+  Split sp = split_on(out, count, esz);
+  a.out = (char *)out;
+  a.npkt = sp.npkt;
+  a.head = sp.head;
+  a.tail = sp.tail;
+  a.n = (uint32_t)n;
+  const uint64_t tile = (uint64_t)c.block * c.unroll;
+  a.ntiles = tiles_for(sp.npkt, tile);
+  for (int k = 0; k < n; k++) a.in[k] = (const char *)in[k];
+
+  const int dev = current_device();
+  uint64_t grid = (uint64_t)device_cus(dev) * c.bpc;
+  if (grid > a.ntiles) grid = a.ntiles;
+  fn(a, dim3((unsigned)grid), s);
+  return check_hip(hipGetLastError(), "hiccl_reduce: launch");
+}
+
+int hiccl_reduce(int dtype, void *out, const void *const *in, int n, size_t count, void *stream) {
+  return hiccl_reduce_ex(dtype, out, in, n, count, stream, nullptr);
+}
+
+int hiccl_reduce_f32(float *out, const float *const *in, int n, size_t count, void *stream) {
+  return hiccl_reduce_ex(HICCL_FLOAT32, out, (const void *const *)in, n, count, stream, nullptr);
+}
+
+int hiccl_reduce_bf16(uint16_t *out, const uint16_t *const *in, int n, size_t count,
+                      void *stream) {
+  return hiccl_reduce_ex(HICCL_BFLOAT16, out, (const void *const *)in, n, count, stream, nullptr);
+}
+
+// ---------------------------------------------------------------- plan ----
+
+}  // extern "C"
+
+struct hiccl_reduce_plan {
+  int dtype = 0;
+  int device = 0;
+  int acc = HICCL_ACC_NATIVE;
+  size_t esz = 0;
+  struct Comp {
+    void *out;
+    std::vector<const void *> in;
+    size_t count;
+  };
+  std::vector<Comp> comps;
+  std::vector<PlanDesc> host_desc;  // numcomp + 1 (sentinel)
+  int maxn = 0;
+  bool dirty = true;
+  PlanDesc *d_desc = nullptr;
+  const void **d_ptrs = nullptr;
+  uint64_t total_tiles = 0;
+  hipStream_t own = nullptr;
+  hipEvent_t done = nullptr;
+  bool launched = false;
+};
+
+namespace {
+
+int plan_upload(hiccl_reduce_plan *p) {
+  if (!p->dirty) return 0;
+  if (p->d_desc) { (void)hipFree(p->d_desc); p->d_desc = nullptr; }
+  if (p->d_ptrs) { (void)hipFree(p->d_ptrs); p->d_ptrs = nullptr; }
+  const size_t nc = p->comps.size();
+  size_t nptr = 0;
+  for (auto &c : p->comps) nptr += c.in.size();
+  std::vector<const void *> ptrs;
+  ptrs.reserve(nptr ? nptr : 1);
+  for (auto &c : p->comps) ptrs.insert(ptrs.end(), c.in.begin(), c.in.end());
+  if (ptrs.empty()) ptrs.push_back(nullptr);
+  if (int e = check_hip(hipMalloc((void **)&p->d_ptrs, ptrs.size() * sizeof(void *)), "plan: hipMalloc ptrs"))
+    return e;
+  if (int e = check_hip(hipMemcpy(p->d_ptrs, ptrs.data(), ptrs.size() * sizeof(void *),
+                                  hipMemcpyHostToDevice), "plan: upload ptrs"))
+    return e;
+  p->host_desc.assign(nc + 1, PlanDesc{});
+  uint64_t tile = 0;
+  size_t off = 0;
+  p->maxn = 0;
+  for (size_t i = 0; i < nc; i++) {
+    auto &c = p->comps[i];
+    Split sp = split_on(c.out, c.count, p->esz);
+    PlanDesc &d = p->host_desc[i];
+    d.out = (char *)c.out;
+    d.in = (const char *const *)(p->d_ptrs + off);
+    d.npkt = sp.npkt;
+    d.head = sp.head;
+    d.tail = sp.tail;
+    d.n = (uint32_t)c.in.size();
+    d.tile_begin = tile;
+    tile += tiles_for(sp.npkt, kPlanTile);
+    off += c.in.size();
+    if ((int)c.in.size() > p->maxn) p->maxn = (int)c.in.size();
+  }
+  p->host_desc[nc].tile_begin = UINT64_MAX;  // sentinel
+  p->total_tiles = tile;
+  if (int e = check_hip(hipMalloc((void **)&p->d_desc, (nc + 1) * sizeof(PlanDesc)), "plan: hipMalloc desc"))
+    return e;
+  if (int e = check_hip(hipMemcpy(p->d_desc, p->host_desc.data(), (nc + 1) * sizeof(PlanDesc),
+                                  hipMemcpyHostToDevice), "plan: upload desc"))
+    return e;
+  p->dirty = false;
+  return 0;
+}
+
+int plan_kernel(hiccl_reduce_plan *p, uint32_t c0, uint64_t t0, uint64_t t1, int maxn,
+                hipStream_t s) {
+  plan_fn fn = pick_plan(p->dtype, p->acc);
+  if (!fn) return fail(hipErrorInvalidValue, "plan: unsupported dtype");
+  uint64_t grid = (uint64_t)device_cus(p->device) * 8;
+  if (grid > t1 - t0) grid = t1 - t0;
+  fn(p->d_desc, c0, t0, t1, dim3((unsigned)grid), s);
+  return check_hip(hipGetLastError(), "plan: launch");
+}
+
+int reduce_via_table(int dtype, int acc, void *out, const void *const *in, int n, size_t count,
+                     hipStream_t s) {
+  const size_t esz = esize(dtype);
+  Split sp = split_on(out, count, esz);
+  const size_t bytes = 2 * sizeof(PlanDesc) + (size_t)n * sizeof(void *);
+  std::vector<char> host(bytes, 0);
+  PlanDesc *hd = (PlanDesc *)host.data();
+  const void **hp = (const void **)(host.data() + 2 * sizeof(PlanDesc));
+  for (int k = 0; k < n; k++) hp[k] = in[k];
+  char *dmem = nullptr;
+  if (int e = check_hip(hipMallocAsync((void **)&dmem, bytes, s), "hiccl_reduce: hipMallocAsync"))
+    return e;
+  hd[0].out = (char *)out;
+  hd[0].in = (const char *const *)(dmem + 2 * sizeof(PlanDesc));
+  hd[0].npkt = sp.npkt;
+  hd[0].head = sp.head;
+  hd[0].tail = sp.tail;
+  hd[0].n = (uint32_t)n;
+  hd[0].tile_begin = 0;
+  const uint64_t tiles = tiles_for(sp.npkt, kPlanTile);
+  hd[1].tile_begin = UINT64_MAX;
+  if (int e = check_hip(hipMemcpyAsync(dmem, host.data(), bytes, hipMemcpyHostToDevice, s),
+                        "hiccl_reduce: table upload"))
+    return e;
+  plan_fn fn = pick_plan(dtype, acc);
+  uint64_t grid = (uint64_t)device_cus(current_device()) * 8;
+  if (grid > tiles) grid = tiles;
+  fn((const PlanDesc *)dmem, 0, 0, tiles, dim3((unsigned)grid), s);
+  if (int e = check_hip(hipGetLastError(), "hiccl_reduce: launch")) return e;
+  return check_hip(hipFreeAsync(dmem, s), "hiccl_reduce: hipFreeAsync");
+}
+
+}  // namespace
+
+extern "C" {
+
+int hiccl_reduce_plan_create(hiccl_reduce_plan_t **plan, int dtype, int device) {
+  if (!plan) return fail(hipErrorInvalidValue, "plan_create: plan is NULL");
+  *plan = nullptr;
+  if (!esize(dtype)) return fail(hipErrorInvalidValue, "plan_create: unknown dtype");
+  int ndev = 0;
+  if (int e = check_hip(hipGetDeviceCount(&ndev), "plan_create: hipGetDeviceCount")) return e;
+  if (device < 0 || device >= ndev) return fail(hipErrorInvalidDevice, "plan_create: bad device");
+  if (int e = check_hip(hipSetDevice(device), "plan_create: hipSetDevice")) return e;
+  auto *p = new hiccl_reduce_plan;
+  p->dtype = dtype;
+  p->device = device;
+  p->esz = esize(dtype);
+  if (int e = check_hip(hipStreamCreateWithFlags(&p->own, hipStreamNonBlocking), "plan_create: stream")) {
+    delete p;
+    return e;
+  }
+  if (int e = check_hip(hipEventCreateWithFlags(&p->done, hipEventDisableTiming), "plan_create: event")) {
+    (void)hipStreamDestroy(p->own);
+    delete p;
+    return e;
+  }
+  *plan = p;
+  return 0;
+}
+
+int hiccl_reduce_plan_set_acc(hiccl_reduce_plan_t *p, int acc) {
+  if (!p) return fail(hipErrorInvalidValue, "plan_set_acc: plan is NULL");
+  if (acc != HICCL_ACC_NATIVE && acc != HICCL_ACC_WIDE)
+    return fail(hipErrorInvalidValue, "plan_set_acc: bad mode");
+  p->acc = acc;
+  return 0;
+}
+
+int hiccl_reduce_plan_add(hiccl_reduce_plan_t *p, void *out, const void *const *in, int n,
+                          size_t count) {
+  if (!p) return fail(hipErrorInvalidValue, "plan_add: plan is NULL");
+  if (int e = check_buffers(out, in, n, count, p->esz)) return e;
+  if (count == 0) return 0;
+  hiccl_reduce_plan::Comp c;
+  c.out = out;
+  c.in.assign(in, in + n);
+  c.count = count;
+  p->comps.push_back(std::move(c));
+  p->dirty = true;
+  return 0;
+}
+
+int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *p, void *stream) {
+  if (!p) return fail(hipErrorInvalidValue, "plan_launch: plan is NULL");
+  if (int e = check_hip(hipSetDevice(p->device), "plan_launch: hipSetDevice")) return e;
+  if (p->comps.empty()) return 0;
+  if (int e = plan_upload(p)) return e;
+  hipStream_t s = stream ? (hipStream_t)stream : p->own;
+  if (int e = plan_kernel(p, 0, 0, p->total_tiles, p->maxn, s)) return e;
+  p->launched = true;
+  return check_hip(hipEventRecord(p->done, s), "plan_launch: event");
+}
+
+int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *p, void *stream) {
+  if (!p) return fail(hipErrorInvalidValue, "plan_launch_each: plan is NULL");
+  if (int e = check_hip(hipSetDevice(p->device), "plan_launch_each: hipSetDevice")) return e;
+  if (p->comps.empty()) return 0;
+  if (int e = plan_upload(p)) return e;
+  hipStream_t s = stream ? (hipStream_t)stream : p->own;
+  for (size_t c = 0; c < p->comps.size(); c++) {
+    const uint64_t t0 = p->host_desc[c].tile_begin;
+    const uint64_t t1 = (c + 1 < p->comps.size()) ? p->host_desc[c + 1].tile_begin : p->total_tiles;
+    if (int e = plan_kernel(p, (uint32_t)c, t0, t1, (int)p->comps[c].in.size(), s)) return e;
+  }
+  p->launched = true;
+  return check_hip(hipEventRecord(p->done, s), "plan_launch_each: event");
+}
+
+int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *p) {
+  if (!p) return fail(hipErrorInvalidValue, "plan_sync: plan is NULL");
+  if (!p->launched) return 0;
+  if (int e = check_hip(hipSetDevice(p->device), "plan_sync: hipSetDevice")) return e;
+  return check_hip(hipEventSynchronize(p->done), "plan_sync");
+}
+
+int hiccl_reduce_plan_numcomp(const hiccl_reduce_plan_t *p) { return p ? (int)p->comps.size() : 0; }
+
+size_t hiccl_reduce_plan_bytes(const hiccl_reduce_plan_t *p) {
+  if (!p) return 0;
+  size_t b = 0;
+  for (auto &c : p->comps) b += c.count * (c.in.size() + 1) * p->esz;
+  return b;
+}
+
+void hiccl_reduce_plan_destroy(hiccl_reduce_plan_t *p) {
+  if (!p) return;
+  (void)hipSetDevice(p->device);
+  if (p->launched) (void)hipEventSynchronize(p->done);
+  if (p->d_desc) (void)hipFree(p->d_desc);
+  if (p->d_ptrs) (void)hipFree(p->d_ptrs);
+  if (p->done) (void)hipEventDestroy(p->done);
+  if (p->own) (void)hipStreamDestroy(p->own);
+  delete p;
+}
+
+// ---------------------------------------------------------- measurement --
+
+int hiccl_fill_uniform(int dtype, void *out, size_t count, uint64_t seed, uint32_t k, size_t first,
+                       void *stream) {
+  if (count == 0) return 0;
+  if (!out) return fail(hipErrorInvalidValue, "fill_uniform: out is NULL");
+  // Same key derivation as oracle/reduce_oracle.c hash3(): splitmix64(seed ^ k<<48) + i.
+  uint64_t z = seed ^ ((uint64_t)k << 48);
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  const uint64_t key = z ^ (z >> 31);
+  uint64_t blocks = (count + 255) / 256;
+  const uint64_t cap = (uint64_t)device_cus(current_device()) * 16;
+  if (blocks > cap) blocks = cap;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dtype) {
+    case HICCL_FLOAT32:
+      hipLaunchKernelGGL(k_fill<HICCL_FLOAT32>, dim3((unsigned)blocks), dim3(256), 0, s, (char *)out,
+                         (uint64_t)count, key, (uint64_t)first);
+      break;
+    case HICCL_FLOAT64:
+      hipLaunchKernelGGL(k_fill<HICCL_FLOAT64>, dim3((unsigned)blocks), dim3(256), 0, s, (char *)out,
+                         (uint64_t)count, key, (uint64_t)first);
+      break;
+    case HICCL_BFLOAT16:
+      hipLaunchKernelGGL(k_fill<HICCL_BFLOAT16>, dim3((unsigned)blocks), dim3(256), 0, s, (char *)out,
+                         (uint64_t)count, key, (uint64_t)first);
+      break;
+    default: return fail(hipErrorInvalidValue, "fill_uniform: dtype must be FLOAT32/FLOAT64/BFLOAT16");
+  }
+  return check_hip(hipGetLastError(), "fill_uniform: launch");
+}
+
+int hiccl_stream_copy(void *dst, const void *src, size_t bytes, void *stream) {
+  if (bytes == 0) return 0;
+  if (!dst || !src) return fail(hipErrorInvalidValue, "stream_copy: NULL pointer");
+  if ((uintptr_t)dst % 16 || (uintptr_t)src % 16)
+    return fail(hipErrorInvalidValue, "stream_copy: pointers must be 16-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t npkt = bytes / 16;
+  if (npkt) {
+    uint64_t blocks = (npkt + 1023) / 1024;
+    const uint64_t cap = (uint64_t)device_cus(current_device()) * 8;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(k_copy, dim3((unsigned)blocks), dim3(256), 0, s, (u32x4 *)dst,
+                       (const u32x4 *)src, npkt);
+  }
+  if (bytes % 16)
+    hipLaunchKernelGGL(k_copy_bytes, dim3(1), dim3(64), 0, s, (char *)dst + npkt * 16,
+                       (const char *)src + npkt * 16, (uint64_t)(bytes % 16));
+  return check_hip(hipGetLastError(), "stream_copy: launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,149 @@
+/*
+ * hiccl_reduce.h -- C ABI of the MI355X (gfx950) bucket-reduction stage.
+ *
+ * This is the drop-in boundary for HiCCL's local reduction compute stage:
+ * element-wise, in-order sum of N gathered device buffers into one output,
+ *
+ *     out[i] = ((((T)0 + in[0][i]) + in[1][i]) + ...) + in[n-1][i]
+ *
+ * with every add rounded to T (reference: source/compute.h:2-12 GPU
+ * reduce_kernel<T>, compute.h:14-23 CPU reduce_kernel<T>).  Results are
+ * bit-identical to the reference's reduction on the same inputs.
+ *
+ * Plain C: pointers, sizes and ints only.  `stream` is a hipStream_t passed
+ * as void* (NULL = the default stream), device pointers are plain void*.
+ * Every function returns a hipError_t value as int (0 = hipSuccess); invalid
+ * arguments return hipErrorInvalidValue (1) and leave a message readable with
+ * hiccl_last_error().
+ *
+ * Implementation: hiccl_amd/csrc/reduce.hip -> hiccl_amd/libhiccl_reduce.so
+ * Design and roofline: DESIGN.md.  Reference-side bindings: INTEGRATION.md.
+ */
+#ifndef HICCL_REDUCE_H
+#define HICCL_REDUCE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Element types.  The reference is a template over T (compute.h:26); its
+ * drivers instantiate T = size_t (collectives/main.cpp:24, main.cpp:4) and
+ * T = float (main.cu:10).  bf16 follows `T acc; acc += x` semantics
+ * (round to bf16 after every add) unless HICCL_ACC_WIDE is requested. */
+typedef enum {
+  HICCL_FLOAT32 = 0,
+  HICCL_FLOAT64 = 1,
+  HICCL_BFLOAT16 = 2,
+  HICCL_UINT64 = 3, /* size_t */
+  HICCL_INT32 = 4,
+  HICCL_NUM_DTYPES = 5
+} hiccl_dtype_t;
+
+/* Accumulation mode (only meaningful for HICCL_BFLOAT16). */
+typedef enum {
+  HICCL_ACC_NATIVE = 0, /* accumulate in T: reference semantics (default) */
+  HICCL_ACC_WIDE = 1    /* accumulate bf16 in f32, round once: NOT reference-bitwise */
+} hiccl_acc_t;
+
+/* Size in bytes of one element of `dtype`, 0 if unknown. */
+size_t hiccl_dtype_size(int dtype);
+
+/* Message describing the last error returned on this host thread. */
+const char *hiccl_last_error(void);
+
+/* Library version as MAJOR*10000 + MINOR*100 + PATCH. */
+int hiccl_version(void);
+
+/* ----------------------------------------------------------------------
+ * One-shot reduction.  Replaces one registered compute of the reference's
+ * Compute<T> being launched: compute.h:145 (launch of reduce_kernel with
+ * the device pointer table built at compute.h:124-126).
+ *
+ *   in     HOST array of n DEVICE pointers, in summation order (the order
+ *          reduce.h:134-169 emits: ascending rank).  Copied at call time;
+ *          the caller may free it on return.
+ *   out    device pointer; may equal one of the inputs exactly (in-place);
+ *          partial overlap with an input is not allowed.
+ *   count  elements; 0 is a no-op.  n == 0 writes T(0) to every element.
+ *   Pointers need only be element-aligned; inputs may be mutually
+ *   misaligned (element offsets from reduce.h:401-415 partition()).
+ *   Asynchronous on `stream`.
+ */
+int hiccl_reduce(int dtype, void *out, const void *const *in, int n, size_t count,
+                 void *stream);
+int hiccl_reduce_f32(float *out, const float *const *in, int n, size_t count, void *stream);
+int hiccl_reduce_bf16(uint16_t *out, const uint16_t *const *in, int n, size_t count,
+                      void *stream);
+
+/* Tuning knobs of the single-compute kernel.  Zero fields mean "default". */
+typedef struct {
+  int block;         /* threads per workgroup: 256 or 512 */
+  int unroll;        /* 16-byte packets per input per lane per tile: 1, 2 or 4 */
+  int blocks_per_cu; /* persistent grid = CUs x this (capped by tiles) */
+  int nontemporal;   /* 0 plain, 1 nt loads, 2 nt loads + nt stores */
+  int acc;           /* hiccl_acc_t */
+} hiccl_reduce_config_t;
+
+int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t count,
+                    void *stream, const hiccl_reduce_config_t *cfg);
+
+/* ----------------------------------------------------------------------
+ * Persistent plan: the C-ABI counterpart of the reference's Compute<T>
+ * (compute.h:26-204).  A plan holds any number of registered computes and
+ * launches ALL of them in ONE kernel (one launch per pipeline step instead
+ * of one launch + one stream per compute, compute.h:141-159).
+ *
+ *   create   compute.h:26 (object) -- binds `device`.
+ *   add      compute.h:101-139 add(inputbuf, outputbuf, count, compid):
+ *            records one compute; `in` is a HOST array of n DEVICE
+ *            pointers, copied.  (The reference's SPMD "only if myid ==
+ *            compid" filter is applied by the C++ caller.)
+ *   launch   compute.h:141-160 start(): one batched kernel on `stream`
+ *            (NULL = the plan's own stream).  The first launch after an add
+ *            uploads the descriptor table (synchronous, once).
+ *   sync     compute.h:161-171 wait(): blocks until the plan's last launch
+ *            has completed.
+ *   destroy  frees the plan's device tables and stream (the reference leaks
+ *            them, compute.h:124-137).
+ * Threading: launch/sync may be called from a different host thread than
+ * create/add (Comm::start's pthread, comm.h:214-224); each entry binds the
+ * plan's device.  Not reentrant per plan; distinct plans are independent.
+ */
+typedef struct hiccl_reduce_plan hiccl_reduce_plan_t;
+
+int hiccl_reduce_plan_create(hiccl_reduce_plan_t **plan, int dtype, int device);
+int hiccl_reduce_plan_set_acc(hiccl_reduce_plan_t *plan, int acc);
+int hiccl_reduce_plan_add(hiccl_reduce_plan_t *plan, void *out, const void *const *in, int n,
+                          size_t count);
+int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *plan, void *stream);
+/* Reference structure, for measurement: one kernel per compute, each on
+ * the given stream (compute.h:141-145 launches one kernel per compute). */
+int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *plan, void *stream);
+int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *plan);
+int hiccl_reduce_plan_numcomp(const hiccl_reduce_plan_t *plan);
+/* Sum over computes of count * (n + 1) * sizeof(T): the bytes the reference's
+ * measure(warmup, numiter) overload (compute.h:251-257) prices. */
+size_t hiccl_reduce_plan_bytes(const hiccl_reduce_plan_t *plan);
+void hiccl_reduce_plan_destroy(hiccl_reduce_plan_t *plan);
+
+/* ----------------------------------------------------------------------
+ * Measurement utilities (bench.py; not part of the reference surface).
+ *
+ * fill_uniform: element i of buffer k = uniform [-1,1) value of hash
+ * (seed, k, first + i), identical to oracle/reduce_oracle.c's generator
+ * (dtypes FLOAT32, BFLOAT16, FLOAT64).
+ * stream_copy: plain 16-byte-per-lane device copy, the achievable-bandwidth
+ * ceiling reference for the roofline.
+ */
+int hiccl_fill_uniform(int dtype, void *out, size_t count, uint64_t seed, uint32_t k,
+                       size_t first, void *stream);
+int hiccl_stream_copy(void *dst, const void *src, size_t bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HICCL_REDUCE_H */

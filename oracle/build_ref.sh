@@ -1,0 +1,38 @@
+#!/usr/bin/env bash
+# oracle/build_ref.sh -- TEST INFRASTRUCTURE ONLY.
+#
+# Compiles the reference's OWN CPU reduction, reduce_kernel<T>
+# (/root/reference/source/compute.h:14-23, the branch taken when no PORT_*
+# macro is defined), into oracle/_ref/libhiccl_ref.so.  The function is
+# read straight out of the reference header (the lines between the first
+# `#else` and `#endif` of compute.h) and piped to g++ on stdin, so no
+# reference source is ever written into this repository.  The fragment
+# needs nothing but <cstddef> (size_t) -- no CommBench, no MPI, no stand-in
+# headers: the rest of HiCCL (whose CommBench submodule is not vendored,
+# .gitmodules:1-3) is NOT built.  It is wrapped in `namespace HiCCL` exactly
+# as hiccl.h:29,43 includes it, and explicitly instantiated for the types the
+# reference drivers use (float: main.cu:10; size_t: collectives/main.cpp:24)
+# plus double.
+#
+# usage: build_ref.sh <reference-root> <output.so>
+set -euo pipefail
+REF=${1:-/root/reference}
+OUT=${2:-$(dirname "$0")/_ref/libhiccl_ref.so}
+SRC="$REF/source/compute.h"
+[ -f "$SRC" ] || { echo "build_ref: $SRC not found (reference absent) -- skipping" >&2; exit 0; }
+mkdir -p "$(dirname "$OUT")"
+FRAG=$(awk '/^#else/{f=1;next} /^#endif/{if(f)exit} f' "$SRC")
+grep -q 'void reduce_kernel' <<<"$FRAG" || { echo "build_ref: reduce_kernel not found in $SRC" >&2; exit 1; }
+{
+  echo '#include <cstddef>'
+  echo '#include <cstdint>'
+  echo 'namespace HiCCL {'
+  echo "#line 14 \"$SRC\""
+  echo "$FRAG"
+  echo '}'
+  echo '#line 1 "oracle/build_ref.sh:wrapper"'
+  echo 'extern "C" void ref_reduce_f32(float *o, size_t c, float **in, int n) { HiCCL::reduce_kernel<float>(o, c, in, n); }'
+  echo 'extern "C" void ref_reduce_f64(double *o, size_t c, double **in, int n) { HiCCL::reduce_kernel<double>(o, c, in, n); }'
+  echo 'extern "C" void ref_reduce_u64(size_t *o, size_t c, size_t **in, int n) { HiCCL::reduce_kernel<size_t>(o, c, in, n); }'
+} | g++ -x c++ -std=c++17 -O3 -fopenmp -fPIC -shared -o "$OUT" -
+echo "build_ref: built $OUT from $SRC"

@@ -1,0 +1,78 @@
+"""CPU tier: the C-ABI library loads, exports every declared symbol, and its
+host-side argument checking behaves (no compute calls without a GPU)."""
+import ctypes
+import os
+
+import pytest
+
+import hiccl_amd
+from hiccl_amd import _lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_built_in_tree():
+    assert os.path.exists(L.LIB_PATH), "run make / __graft_entry__.build()"
+    assert os.path.dirname(L.LIB_PATH) == os.path.join(ROOT, "hiccl_amd")
+
+
+def test_exports_every_header_symbol():
+    names = L.header_functions()
+    assert "hiccl_reduce" in names and "hiccl_reduce_plan_launch" in names
+    raw = ctypes.CDLL(L.LIB_PATH)
+    missing = [n for n in names if not hasattr(raw, n)]
+    assert not missing, f"declared in include/hiccl_reduce.h but not exported: {missing}"
+    # and every declared symbol has a Python signature
+    assert not [n for n in names if n not in L._SIGS]
+
+
+def test_gfx950_code_object_embedded():
+    blob = open(L.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_dtype_sizes_and_version():
+    lib = L.lib()
+    assert [lib.hiccl_dtype_size(d) for d in range(5)] == [4, 8, 2, 8, 4]
+    assert lib.hiccl_dtype_size(99) == 0
+    assert lib.hiccl_version() >= 100
+
+
+def _tab(ptrs):
+    return (ctypes.c_void_p * max(1, len(ptrs)))(*ptrs)
+
+
+def test_invalid_arguments_rejected_on_host():
+    lib = L.lib()
+    # unknown dtype
+    assert lib.hiccl_reduce(42, ctypes.c_void_p(0x1000), _tab([0x2000]), 1, 4, None) == 1
+    assert "dtype" in L.last_error()
+    # count == 0 is a no-op (no device access)
+    assert lib.hiccl_reduce(0, ctypes.c_void_p(0), _tab([]), 0, 0, None) == 0
+    # NULL out
+    assert lib.hiccl_reduce(0, ctypes.c_void_p(0), _tab([0x2000]), 1, 4, None) == 1
+    assert "out is NULL" in L.last_error()
+    # misaligned out for f32
+    assert lib.hiccl_reduce(0, ctypes.c_void_p(0x1002), _tab([0x2000]), 1, 4, None) == 1
+    assert "element-aligned" in L.last_error()
+    # NULL input pointer
+    assert lib.hiccl_reduce(0, ctypes.c_void_p(0x1000), _tab([0]), 1, 4, None) == 1
+    # partial overlap of an input with the output (exact aliasing is allowed)
+    assert lib.hiccl_reduce(0, ctypes.c_void_p(0x1000), _tab([0x1004]), 1, 4, None) == 1
+    assert "overlaps" in L.last_error()
+    # negative n
+    assert lib.hiccl_reduce(0, ctypes.c_void_p(0x1000), _tab([]), -1, 4, None) == 1
+    # unsupported tuning config
+    cfg = L.ReduceConfig(block=128)
+    assert lib.hiccl_reduce_ex(0, ctypes.c_void_p(0x1000), _tab([0x2000]), 1, 4, None, ctypes.byref(cfg)) == 1
+    # plan NULL handling
+    assert lib.hiccl_reduce_plan_launch(None, None) == 1
+    assert lib.hiccl_reduce_plan_numcomp(None) == 0
+    lib.hiccl_reduce_plan_destroy(None)
+
+
+def test_python_layer_refuses_cpu_tensors():
+    import torch
+    x = torch.zeros(4)
+    with pytest.raises(ValueError, match="device tensor"):
+        hiccl_amd.reduce(x, [x])

@@ -1,0 +1,260 @@
+"""GPU tier: the HIP kernels through the C ABI vs the oracle and the golden
+fixtures (bit-exact; NaN outputs compared by NaN-ness).
+
+Covers the edge cases SURVEY.md sections 4 and 8a list: n = 0, 1, 2, 3, 4, 7,
+8, 9, 16, 64 and > 64 (device pointer table), counts around the packet/tile
+boundaries, signed zeros / Inf / NaN / denormals / overflow, mutually
+misaligned inputs (partition() element offsets), in-place outputs, bf16 in
+both accumulation modes, size_t known-answer, the batched plan vs the
+reference's one-launch-per-compute structure, and a full-size sampled check.
+"""
+import numpy as np
+import pytest
+import torch
+
+import hiccl_amd
+from conftest import bits_equal, first_mismatch, load_golden
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+TORCH_OF = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+            np.dtype(np.uint64): torch.int64, np.dtype(np.uint16): torch.bfloat16}
+
+
+def to_dev(a):
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint16:
+        return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16).to(DEV)
+    if a.dtype == np.uint64:
+        return torch.from_numpy(a.view(np.int64).copy()).to(DEV)
+    return torch.from_numpy(a.copy()).to(DEV)
+
+
+def to_host(t, np_dtype):
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).cpu().numpy().view(np.uint16)
+    if np.dtype(np_dtype) == np.uint64:
+        return t.cpu().numpy().view(np.uint64)
+    return t.cpu().numpy()
+
+
+def gpu_reduce(x, count, dtype, offsets=None, out_offset=0, config=None):
+    """Place each input row at an element offset inside its own buffer and
+    reduce; returns the host result."""
+    n = x.shape[0]
+    tdt = TORCH_OF[np.dtype(dtype)]
+    offsets = offsets or [0] * n
+    bufs = []
+    ins = []
+    for k in range(n):
+        b = torch.empty(count + offsets[k] + 8, dtype=tdt, device=DEV)
+        b.view(torch.uint8).fill_(0x5A)
+        seg = b[offsets[k]:offsets[k] + count]
+        seg.copy_(to_dev(x[k]).view(tdt) if count else seg)
+        bufs.append(b)
+        ins.append(seg)
+    ob = torch.empty(count + out_offset + 8, dtype=tdt, device=DEV)
+    ob.view(torch.uint8).fill_(0xA5)
+    out = ob[out_offset:out_offset + count]
+    hiccl_amd.reduce(out, ins, count=count, config=config)
+    torch.cuda.synchronize()
+    # guard bytes around the output must be untouched
+    guard = to_host(ob, dtype)
+    assert (guard[:out_offset].view(np.uint8) == 0xA5).all()
+    assert (guard[out_offset + count:].view(np.uint8) == 0xA5).all()
+    return to_host(out, dtype)
+
+
+@pytest.mark.parametrize("name,dtype", [("reduce_f32", np.float32), ("reduce_f64", np.float64),
+                                        ("reduce_u64", np.uint64), ("reduce_bf16", np.uint16)])
+def test_golden_fixtures(name, dtype):
+    for case, d in load_golden(name).items():
+        x, y = d["in"], d["out"]
+        got = gpu_reduce(x, len(y), dtype)
+        assert bits_equal(got, y), f"{name}/{case}: {first_mismatch(got, y)}"
+
+
+@pytest.mark.parametrize("offs", [[1, 0], [0, 3], [1, 2, 3, 0], [3, 3, 3], [2, 1, 0, 3, 2, 1, 0, 3, 1]])
+@pytest.mark.parametrize("out_off", [0, 1, 3])
+def test_misaligned_inputs_f32(oracle, offs, out_off):
+    n = len(offs)
+    for count in (1, 5, 4099, 70001):
+        x = oracle.fill(n, count, seed=11 + count)
+        got = gpu_reduce(x, count, np.float32, offsets=offs, out_offset=out_off)
+        exp = oracle.reduce(list(x))
+        assert bits_equal(got, exp), f"offs={offs} out={out_off} count={count}: {first_mismatch(got, exp)}"
+
+
+@pytest.mark.parametrize("offs", [[1, 0, 5], [7, 3], [0, 0, 1, 2, 3, 4, 5, 6]])
+def test_misaligned_inputs_bf16(oracle, offs):
+    n = len(offs)
+    for count in (3, 9, 4099, 33333):
+        x = oracle.fill(n, count, seed=5, dtype=np.uint16)
+        got = gpu_reduce(x, count, np.uint16, offsets=offs, out_offset=1)
+        exp = oracle.reduce(list(x), dtype=np.uint16)
+        assert bits_equal(got, exp), f"offs={offs} count={count}: {first_mismatch(got, exp)}"
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 5, 6, 7, 8, 9, 15, 16, 17, 31, 64, 65, 100, 200])
+def test_input_counts(oracle, n):
+    count = 3 * 4096 + 77
+    x = oracle.fill(n, count, seed=n) if n else np.zeros((0, count), np.float32)
+    got = gpu_reduce(x, count, np.float32)
+    exp = oracle.reduce(list(x), count=count, dtype=np.float32)
+    assert bits_equal(got, exp), f"n={n}: {first_mismatch(got, exp)}"
+
+
+@pytest.mark.parametrize("count", [1, 2, 3, 4, 5, 511, 512, 513, 2047, 2048, 2049, 8191, 8192, 8193,
+                                   131072 * 4 + 3])
+def test_tile_boundaries(oracle, count):
+    x = oracle.fill(4, count, seed=3)
+    got = gpu_reduce(x, count, np.float32)
+    assert bits_equal(got, oracle.reduce(list(x)))
+
+
+@pytest.mark.parametrize("config", [
+    dict(block=256, unroll=1), dict(block=256, unroll=2), dict(block=256, unroll=4),
+    dict(block=512, unroll=1), dict(block=512, unroll=2), dict(block=512, unroll=4),
+    dict(block=256, unroll=2, nontemporal=1), dict(block=256, unroll=2, nontemporal=2),
+    dict(block=512, unroll=4, nontemporal=2, blocks_per_cu=2)])
+def test_tuning_variants_same_bits(oracle, config):
+    for n, count in ((8, 1 << 20), (3, 123457)):
+        x = oracle.fill(n, count, seed=n)
+        got = gpu_reduce(x, count, np.float32, offsets=[0, 1] + [0] * (n - 2), config=config)
+        assert bits_equal(got, oracle.reduce(list(x))), config
+        xb = oracle.fill(n, count, seed=n, dtype=np.uint16)
+        gotb = gpu_reduce(xb, count, np.uint16, config=config)
+        assert bits_equal(gotb, oracle.reduce(list(xb), dtype=np.uint16)), config
+
+
+def test_in_place_output(oracle):
+    n, count = 4, 100003
+    x = oracle.fill(n, count, seed=9)
+    ins = [to_dev(r) for r in x]
+    for k in range(n):  # out aliases input k exactly
+        t = [i.clone() for i in ins]
+        hiccl_amd.reduce(t[k], t, count=count)
+        torch.cuda.synchronize()
+        assert bits_equal(t[k].cpu().numpy(), oracle.reduce(list(x))), k
+
+
+def test_in_place_large_n_table_path(oracle):
+    n, count = 80, 20011
+    x = oracle.fill(n, count, seed=1)
+    t = [to_dev(r) for r in x]
+    hiccl_amd.reduce(t[70], t, count=count)
+    torch.cuda.synchronize()
+    assert bits_equal(t[70].cpu().numpy(), oracle.reduce(list(x)))
+
+
+def test_bf16_wide_accumulation(oracle):
+    n, count = 8, 50001
+    x = oracle.fill(n, count, seed=2, dtype=np.uint16)
+    got = gpu_reduce(x, count, np.uint16, config=dict(acc=hiccl_amd.HICCL_ACC_WIDE))
+    exp = oracle.reduce(list(x), dtype=np.uint16, wide=True)
+    assert bits_equal(got, exp), first_mismatch(got, exp)
+
+
+def test_int32_wraparound(oracle):
+    rng = np.random.default_rng(0)
+    x = rng.integers(-2**31, 2**31 - 1, size=(5, 10007), dtype=np.int64).astype(np.int32)
+    ins = [torch.from_numpy(r.copy()).to(DEV) for r in x]
+    out = torch.empty(10007, dtype=torch.int32, device=DEV)
+    hiccl_amd.reduce(out, ins)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), oracle.reduce(list(x)))
+
+
+def test_generator_matches_oracle(oracle):
+    for dtype, tdt in ((np.float32, torch.float32), (np.uint16, torch.bfloat16), (np.float64, torch.float64)):
+        t = torch.empty(100003, dtype=tdt, device=DEV)
+        hiccl_amd.fill_uniform(t, seed=1234, k=5, first=17)
+        torch.cuda.synchronize()
+        exp = oracle.fill(6, 100003, 1234, dtype=dtype, first=17)[5]
+        assert bits_equal(to_host(t, dtype), exp), dtype
+
+
+def _plan_case(oracle, each):
+    rng = np.random.default_rng(4)
+    comp = hiccl_amd.Compute(torch.float32, device=0)
+    expected = []
+    outs = []
+    keep = []
+    for c in range(37):
+        n = int(rng.integers(1, 12))
+        count = int(rng.integers(1, 70000))
+        offs = [int(o) for o in rng.integers(0, 4, size=n)]
+        x = oracle.fill(n, count, seed=100 + c)
+        ins = []
+        for k in range(n):
+            b = torch.empty(count + offs[k], device=DEV)
+            b[offs[k]:].copy_(torch.from_numpy(x[k]))
+            ins.append((b, offs[k]))
+            keep.append(b)
+        ob = torch.full((count + 2,), float("nan"), device=DEV)
+        comp.add(ins, (ob, 1), count, compid=0)
+        outs.append((ob, count))
+        expected.append(oracle.reduce(list(x)))
+    comp.add([(keep[0], 0)], (keep[0], 0), 1, compid=3)  # not mine: ignored (compute.h:120)
+    assert comp.numcomp == 37
+    comp.start(each=each)
+    comp.wait()
+    for (ob, count), exp in zip(outs, expected):
+        got = ob[1:1 + count].cpu().numpy()
+        assert bits_equal(got, exp), first_mismatch(got, exp)
+        assert np.isnan(ob[0].item()) and np.isnan(ob[count + 1].item())
+    # a second launch of the same plan gives the same bits
+    comp.start()
+    comp.wait()
+    assert bits_equal(outs[0][0][1:1 + outs[0][1]].cpu().numpy(), expected[0])
+    comp.close()
+
+
+def test_plan_batched(oracle):
+    _plan_case(oracle, each=False)
+
+
+def test_plan_launch_each(oracle):
+    _plan_case(oracle, each=True)
+
+
+def test_plan_launch_from_other_thread(oracle):
+    """Comm::start runs compute->start() on a pthread (comm.h:214-224)."""
+    import threading
+    x = oracle.fill(3, 4099, seed=8)
+    ins = [to_dev(r) for r in x]
+    out = torch.empty(4099, device=DEV)
+    comp = hiccl_amd.Compute(torch.float32, device=0)
+    comp.add(ins, out, 4099, compid=0)
+    th = threading.Thread(target=lambda: (comp.start(), comp.wait()))
+    th.start()
+    th.join()
+    assert bits_equal(out.cpu().numpy(), oracle.reduce(list(x)))
+
+
+def test_full_size_sampled(oracle):
+    """Config 2 shape (8 x 2^28 f32) checked at 4096 random indices plus the
+    ends: a size-independent property check against the oracle's generator."""
+    n, count, seed = 8, 1 << 28, 1234
+    free, _ = torch.cuda.mem_get_info()
+    if free < (n + 2) * count * 4:
+        pytest.skip("not enough device memory")
+    ins = [torch.empty(count, device=DEV) for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, seed, k)
+    out = torch.empty(count, device=DEV)
+    hiccl_amd.reduce(out, ins)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(0)
+    idx = np.concatenate([np.arange(64), count - 64 + np.arange(64),
+                          rng.integers(0, count, 4096)]).astype(np.int64)
+    got = out[torch.from_numpy(idx).to(DEV)].cpu().numpy()
+    exp = oracle.sample_sum(idx.astype(np.uint64), seed, n)
+    assert bits_equal(got, exp), first_mismatch(got, exp)
+    # checksum-of-checksums: the sum of the output equals the sum of the oracle
+    # partial sums over a strided sample (catches whole-tile drops)
+    stride = 997
+    idx2 = np.arange(0, count, stride * 1024, dtype=np.int64)
+    got2 = out[torch.from_numpy(idx2).to(DEV)].cpu().numpy()
+    assert bits_equal(got2, oracle.sample_sum(idx2.astype(np.uint64), seed, n))
