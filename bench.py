@@ -200,6 +200,24 @@ def cpu_baseline(n, count, budget_s=10.0):
                       f"OpenMP {threads} threads, {cpu_model}"}
 
 
+def sample_check(out, n, count, bf16=False, seed=SEED, nsample=1024):
+    """Bitwise check of `out` at random indices against the oracle generator."""
+    ora_so = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not os.path.exists(ora_so):
+        return None
+    ora = ctypes.CDLL(ora_so)
+    fn = ora.oracle_sample_sum_bf16 if bf16 else ora.oracle_sample_sum_f32
+    fn.restype = None
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int]
+    idx = np.random.default_rng(0).integers(0, count, nsample).astype(np.uint64)
+    idx[:2] = [0, count - 1]
+    exp = np.empty(nsample, np.uint16 if bf16 else np.float32)
+    fn(exp.ctypes.data, idx.ctypes.data, nsample, seed, n)
+    got = out[torch.from_numpy(idx.astype(np.int64)).to(out.device)]
+    got = got.view(torch.int16).cpu().numpy().view(np.uint16) if bf16 else got.cpu().numpy()
+    return bool(np.array_equal(got.view(np.uint8), exp.view(np.uint8)))
+
+
 def traffic_from_profiles(n, count):
     """HBM bytes per launch from a committed PMC summary for this workload."""
     pdir = os.path.join(ROOT, "profiles")
@@ -231,7 +249,9 @@ def main():
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--unroll", type=int, default=0)
     ap.add_argument("--bpc", type=int, default=0)
-    ap.add_argument("--nt", type=int, default=0)
+    ap.add_argument("--nt", type=int, default=-1)
+    ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--store", type=int, default=-1)
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--nway", action="store_true")
     ap.add_argument("--chunks", action="store_true")
@@ -250,8 +270,9 @@ def main():
 
     n, count = args.n, 1 << args.log2count
     cfg = None
-    if args.block or args.unroll or args.bpc or args.nt:
-        cfg = dict(block=args.block, unroll=args.unroll, blocks_per_cu=args.bpc, nontemporal=args.nt)
+    if args.block or args.unroll or args.bpc or args.grid or args.nt >= 0 or args.store >= 0:
+        cfg = dict(block=args.block, unroll=args.unroll, blocks_per_cu=args.bpc, grid=args.grid,
+                   nontemporal=args.nt + 1 if args.nt >= 0 else 0, store_policy=args.store + 1 if args.store >= 0 else 0)
     ins, out = make_bucket(n, count)
     step = lambda: hiccl_amd.reduce(out, ins, config=cfg)  # noqa: E731
     wall, kms = time_launches(step, args.steps, args.warmup, dist)
@@ -320,20 +341,41 @@ def main():
 
 
 def sweep(args):
-    """Interleaved A/B of kernel variants in one process (rule 24)."""
+    """Interleaved A/B of kernel variants in one process (rule 24), with the
+    no-arithmetic 8R+1W probe (tools/libhbm_probe.so) as the ceiling row."""
     n, count = args.n, 1 << args.log2count
     ins, out = make_bucket(n, count)
     variants = []
     for block in (256, 512):
-        for unroll in (1, 2, 4):
-            for nt in (0, 1, 2):
-                for bpc in (0, 2, 4, 8):
-                    variants.append(dict(block=block, unroll=unroll, nontemporal=nt, blocks_per_cu=bpc))
+        for unroll in (2, 4):
+            for nt in (1, 2):
+                for store in (1, 2, 3):
+                    for grid in (192, 256, 512, 1024):
+                        variants.append(dict(block=block, unroll=unroll, nontemporal=nt, store_policy=store,
+                                             grid=grid))
+    probe = None
+    pso = os.path.join(ROOT, "tools", "libhbm_probe.so")
+    if os.path.exists(pso):
+        probe = ctypes.CDLL(pso)
+        probe.probe_run.restype = ctypes.c_int
+        probe.probe_run.argtypes = [ctypes.c_int] * 7 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                         ctypes.c_uint64, ctypes.c_void_p]
+        tab = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ins])
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for g in (192, 256):
+            variants.append(dict(probe=True, block=256, unroll=4, nontemporal=2, store_policy=2, grid=g))
+
+    def runner(v):
+        if v.get("probe"):
+            return lambda: probe.probe_run(0, 256, 4, 2, 2, 0, v["grid"], tab, n, ctypes.c_void_p(out.data_ptr()),
+                                           count * 4, st)
+        return lambda: hiccl_amd.reduce(out, ins, config=v)
+
     res = {i: [] for i in range(len(variants))}
     for rnd in range(3):
         for i, v in enumerate(variants):
             try:
-                _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins, config=v), 5, 2)
+                _, ms = time_launches(runner(v), 5, 2)
             except Exception as e:  # unsupported combination
                 log("skip", v, e)
                 continue
@@ -398,7 +440,9 @@ def chunks(args):
                 t = float(np.median(ms)) * 1e-3
                 res[mode] = t
             b = (n + 1) * count * esz
+            ok = sample_check(out, n, count, bf16=(dtype == torch.bfloat16))
             print(json.dumps({"config": "C4", "dtype": str(dtype).split(".")[-1], "mib_per_input": mib,
+                              "parity_sample_ok": ok,
                               "computes": depth, "batched_ms": round(res["batched"] * 1e3, 4),
                               "batched_GBps": round(b / res["batched"] / 1e9, 1),
                               "each_ms": round(res["each"] * 1e3, 4),

@@ -48,7 +48,7 @@ class HicclError(RuntimeError):
 class ReduceConfig(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("unroll", ctypes.c_int),
                 ("blocks_per_cu", ctypes.c_int), ("nontemporal", ctypes.c_int),
-                ("acc", ctypes.c_int)]
+                ("acc", ctypes.c_int), ("grid", ctypes.c_int), ("store_policy", ctypes.c_int)]
 
 
 _lib = None
@@ -70,6 +70,7 @@ _SIGS = {
     "hiccl_reduce_plan_launch_each": (ctypes.c_int, [_vp, _vp]),
     "hiccl_reduce_plan_sync": (ctypes.c_int, [_vp]),
     "hiccl_reduce_plan_numcomp": (ctypes.c_int, [_vp]),
+    "hiccl_reduce_plan_stream": (_vp, [_vp]),
     "hiccl_reduce_plan_bytes": (ctypes.c_size_t, [_vp]),
     "hiccl_reduce_plan_destroy": (None, [_vp]),
     "hiccl_fill_uniform": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_size_t, ctypes.c_uint64,

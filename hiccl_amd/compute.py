@@ -145,8 +145,14 @@ class Compute:
         self.count.append(count)
         self.numcomp += 1
 
+    def stream_handle(self):
+        """The plan's own stream (hipStream_t as int)."""
+        return L.lib().hiccl_reduce_plan_stream(self._plan)
+
     def start(self, stream=None, each=False):
-        s = _stream_handle(stream) if stream is not None else ctypes.c_void_p(0)
+        """Launch on ``stream`` (torch stream or raw handle); default = the
+        plan's own stream (the reference keeps one per compute, compute.h:131)."""
+        s = _stream_handle(stream) if stream is not None else ctypes.c_void_p(self.stream_handle())
         fn = L.lib().hiccl_reduce_plan_launch_each if each else L.lib().hiccl_reduce_plan_launch
         L.check(fn(self._plan, s), "plan_launch")
 

@@ -82,16 +82,18 @@ __device__ __forceinline__ rsrc_t make_rsrc(const char *base, uint32_t nbytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nbytes, kRsrcFlags);
 }
 
-// Cache policy: NT >= 1 marks loads nontemporal (aux bit 1 = nt), NT >= 2
-// marks stores nontemporal too.
-template <int NT>
+// Cache policy, POL = 10*store + load.  load: 0 default, 1 nt (aux bit 1).
+// store: 0 default, 1 nt, 2 sc1 (aux bit 4: write-through, line dropped
+// from the XCD L2).
+template <int POL>
 __device__ __forceinline__ u32x4 load_pkt(rsrc_t r, uint32_t voff) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, NT >= 1 ? 2 : 0);
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, (POL % 10) == 1 ? 2 : 0);
 }
 
-template <int NT>
+template <int POL>
 __device__ __forceinline__ void store_pkt(rsrc_t r, uint32_t voff, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, 0, NT >= 2 ? 2 : 0);
+  constexpr int sp = POL / 10;
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, 0, sp == 1 ? 2 : sp == 2 ? 16 : 0);
 }
 
 // bf16 <-> f32.  f32 -> bf16 is round-to-nearest-even; on gfx950 the cast
@@ -269,7 +271,7 @@ __device__ __forceinline__ void scalar_part(char *out, Inputs in, uint32_t n, ui
 
 // One group of G inputs (G static): G descriptor builds (scalar), then G*U
 // independent 16-B buffer loads, then the G in-order adds per packet.
-template <class Op, int U, int G, int NT, class Inputs>
+template <class Op, int U, int G, int POL, class Inputs>
 __device__ __forceinline__ void group_at(typename Op::acc_t (&acc)[U], Inputs in, uint32_t g,
                                          uint64_t tile_off, uint32_t tile_bytes,
                                          const uint32_t (&voff)[U]) {
@@ -280,7 +282,7 @@ __device__ __forceinline__ void group_at(typename Op::acc_t (&acc)[U], Inputs in
 #pragma unroll
   for (int j = 0; j < G; j++) {
 #pragma unroll
-    for (int u = 0; u < U; u++) x[j][u] = load_pkt<NT>(r[j], voff[u]);
+    for (int u = 0; u < U; u++) x[j][u] = load_pkt<POL>(r[j], voff[u]);
   }
 #pragma unroll
   for (int j = 0; j < G; j++) {
@@ -293,27 +295,27 @@ __device__ __forceinline__ void group_at(typename Op::acc_t (&acc)[U], Inputs in
 // tile (< the full tile only for the last one).  Inputs are consumed as full
 // groups of 8 followed by one statically sized remainder group, so the adds
 // happen in exactly the order k = 0, 1, ..., n-1.
-template <class Op, int U, int NT, class Inputs>
+template <class Op, int U, int POL, class Inputs>
 __device__ __forceinline__ void tile_body(char *outb, Inputs in, uint32_t n, uint64_t tile_off,
                                           uint32_t tile_bytes, const uint32_t (&voff)[U]) {
   typename Op::acc_t acc[U];
 #pragma unroll
   for (int u = 0; u < U; u++) acc[u] = Op::zero();
   uint32_t g = 0;
-  for (; g + 8 <= n; g += 8) group_at<Op, U, 8, NT>(acc, in, g, tile_off, tile_bytes, voff);
+  for (; g + 8 <= n; g += 8) group_at<Op, U, 8, POL>(acc, in, g, tile_off, tile_bytes, voff);
   switch (n - g) {  // wave-uniform
-    case 1: group_at<Op, U, 1, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 2: group_at<Op, U, 2, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 3: group_at<Op, U, 3, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 4: group_at<Op, U, 4, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 5: group_at<Op, U, 5, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 6: group_at<Op, U, 6, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 7: group_at<Op, U, 7, NT>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 1: group_at<Op, U, 1, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 2: group_at<Op, U, 2, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 3: group_at<Op, U, 3, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 4: group_at<Op, U, 4, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 5: group_at<Op, U, 5, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 6: group_at<Op, U, 6, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 7: group_at<Op, U, 7, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
     default: break;
   }
   rsrc_t w = make_rsrc(outb + tile_off, tile_bytes);
 #pragma unroll
-  for (int u = 0; u < U; u++) store_pkt<NT>(w, voff[u], Op::pack(acc[u]));
+  for (int u = 0; u < U; u++) store_pkt<POL>(w, voff[u], Op::pack(acc[u]));
 }
 
 // Body inputs shifted by the head: base(k) = in[k] + head*esz.
@@ -326,7 +328,7 @@ struct Shifted {
 
 // ------------------------------------------------------------ kernels ------
 
-template <class Op, int BLOCK, int U, int NT>
+template <class Op, int BLOCK, int U, int POL>
 __global__ __launch_bounds__(BLOCK) void k_reduce_single(SingleArgs a) {
   const int tid = threadIdx.x;
   uint32_t voff[U];
@@ -343,7 +345,7 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_single(SingleArgs a) {
     const uint64_t pkt0 = t * TILE;
     const uint64_t left = a.npkt - pkt0;
     const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
-    tile_body<Op, U, NT>(outb, in, a.n, pkt0 * kPacket, tile_bytes, voff);
+    tile_body<Op, U, POL>(outb, in, a.n, pkt0 * kPacket, tile_bytes, voff);
   }
 }
 
@@ -355,7 +357,7 @@ struct TableInputs {
 // All computes of a plan in one launch.  Global tile t belongs to compute c
 // with desc[c].tile_begin <= t < desc[c+1].tile_begin (desc[numdesc] is a
 // sentinel); c only grows along a workgroup's grid-stride walk.
-template <class Op, int BLOCK, int U, int NT>
+template <class Op, int BLOCK, int U, int POL>
 __global__ __launch_bounds__(BLOCK) void k_reduce_plan(const PlanDesc *__restrict__ desc,
                                                        uint32_t c_first, uint64_t t_begin,
                                                        uint64_t t_end) {
@@ -377,7 +379,7 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_plan(const PlanDesc *__restric
     Shifted<TableInputs> in{raw, shift};
     const uint64_t left = d.npkt - pkt0;
     const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
-    tile_body<Op, U, NT>(d.out + shift, in, d.n, pkt0 * kPacket, tile_bytes, voff);
+    tile_body<Op, U, POL>(d.out + shift, in, d.n, pkt0 * kPacket, tile_bytes, voff);
   }
 }
 
@@ -509,18 +511,26 @@ int check_buffers(void *out, const void *const *in, int n, size_t count, size_t 
   return 0;
 }
 
+// Default shape, chosen from on-device sweeps ("Tuning"):
+constexpr int kDefBlock = 256;
+constexpr int kDefUnroll = 4;
+constexpr int kDefPol = 11;  // nt loads, nt stores
+constexpr int kDefBpc = 1;
+
 struct Cfg {
-  int block, unroll, bpc, nt, acc;
+  int block, unroll, bpc, nt, acc, grid, store;
 };
 
 Cfg resolve(const hiccl_reduce_config_t *c) {
-  Cfg r{256, 2, 8, 0, HICCL_ACC_NATIVE};
+  Cfg r{kDefBlock, kDefUnroll, kDefBpc, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10};
   if (c) {
     if (c->block) r.block = c->block;
     if (c->unroll) r.unroll = c->unroll;
     if (c->blocks_per_cu) r.bpc = c->blocks_per_cu;
-    r.nt = c->nontemporal;
+    if (c->nontemporal) r.nt = c->nontemporal - 1;
     r.acc = c->acc;
+    r.grid = c->grid;
+    if (c->store_policy) r.store = c->store_policy - 1;
   }
   return r;
 }
@@ -529,27 +539,30 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
 
 typedef void (*single_fn)(SingleArgs, dim3, hipStream_t);
 
-template <class Op, int B, int U, int NT>
+template <class Op, int B, int U, int POL>
 void launch_single_t(SingleArgs a, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((k_reduce_single<Op, B, U, NT>), grid, dim3(B), 0, s, a);
+  hipLaunchKernelGGL((k_reduce_single<Op, B, U, POL>), grid, dim3(B), 0, s, a);
 }
 
 template <class Op, int B, int U>
-single_fn pick_nt(int nt) {
-  switch (nt) {
+single_fn pick_nt(int pol) {
+  switch (pol) {
     case 0: return launch_single_t<Op, B, U, 0>;
     case 1: return launch_single_t<Op, B, U, 1>;
-    case 2: return launch_single_t<Op, B, U, 2>;
+    case 10: return launch_single_t<Op, B, U, 10>;
+    case 11: return launch_single_t<Op, B, U, 11>;
+    case 20: return launch_single_t<Op, B, U, 20>;
+    case 21: return launch_single_t<Op, B, U, 21>;
     default: return nullptr;
   }
 }
 
 template <class Op, int B>
-single_fn pick_u(int u, int nt) {
+single_fn pick_u(int u, int pol) {
   switch (u) {
-    case 1: return pick_nt<Op, B, 1>(nt);
-    case 2: return pick_nt<Op, B, 2>(nt);
-    case 4: return pick_nt<Op, B, 4>(nt);
+    case 1: return pick_nt<Op, B, 1>(pol);
+    case 2: return pick_nt<Op, B, 2>(pol);
+    case 4: return pick_nt<Op, B, 4>(pol);
     default: return nullptr;
   }
 }
@@ -557,13 +570,14 @@ single_fn pick_u(int u, int nt) {
 // Full tuning table for the headline types; default shape for the rest.
 template <class Op, bool TUNED>
 single_fn pick_single(const Cfg &c) {
+  const int pol = c.store * 10 + c.nt;
   if constexpr (TUNED) {
-    if (c.block == 256) return pick_u<Op, 256>(c.unroll, c.nt);
-    if (c.block == 512) return pick_u<Op, 512>(c.unroll, c.nt);
+    if (c.block == 256) return pick_u<Op, 256>(c.unroll, pol);
+    if (c.block == 512) return pick_u<Op, 512>(c.unroll, pol);
     return nullptr;
   } else {
-    if (c.block != 256 || c.unroll != 2 || c.nt != 0) return nullptr;
-    return launch_single_t<Op, 256, 2, 0>;
+    if (c.block != kDefBlock || c.unroll != kDefUnroll || pol != kDefPol) return nullptr;
+    return launch_single_t<Op, kDefBlock, kDefUnroll, kDefPol>;
   }
 }
 
@@ -582,16 +596,17 @@ single_fn pick_single_dtype(int dtype, const Cfg &c) {
 
 // ---- plan dispatch (default tile shape)
 
-constexpr int kPlanBlock = 256;
-constexpr int kPlanUnroll = 2;
+constexpr int kPlanBlock = kDefBlock;
+constexpr int kPlanUnroll = kDefUnroll;
 constexpr uint64_t kPlanTile = (uint64_t)kPlanBlock * kPlanUnroll;
+constexpr int kPlanBpc = 1;
 
 typedef void (*plan_fn)(const PlanDesc *, uint32_t, uint64_t, uint64_t, dim3, hipStream_t);
 
 template <class Op>
 void launch_plan_t(const PlanDesc *d, uint32_t c0, uint64_t t0, uint64_t t1, dim3 grid,
                    hipStream_t s) {
-  hipLaunchKernelGGL((k_reduce_plan<Op, kPlanBlock, kPlanUnroll, 0>), grid, dim3(kPlanBlock), 0, s,
+  hipLaunchKernelGGL((k_reduce_plan<Op, kPlanBlock, kPlanUnroll, kDefPol>), grid, dim3(kPlanBlock), 0, s,
                      d, c0, t0, t1);
 }
 
@@ -647,8 +662,10 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
     return fail(hipErrorInvalidValue, "hiccl_reduce_ex: unsupported config (block " +
                                           std::to_string(c.block) + ", unroll " +
                                           std::to_string(c.unroll) + ", nt " +
-                                          std::to_string(c.nt) + ") for this dtype");
+                                          std::to_string(c.nt) + ", store " +
+                                          std::to_string(c.store) + ") for this dtype");
   if (c.bpc < 1 || c.bpc > 64) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: blocks_per_cu");
+  if (c.grid < 0) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: grid < 0");
 
   SingleArgs a;
   memset(&a, 0, sizeof(a));
@@ -663,7 +680,7 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
   for (int k = 0; k < n; k++) a.in[k] = (const char *)in[k];
 
   const int dev = current_device();
-  uint64_t grid = (uint64_t)device_cus(dev) * c.bpc;
+  uint64_t grid = c.grid > 0 ? (uint64_t)c.grid : (uint64_t)device_cus(dev) * c.bpc;
   if (grid > a.ntiles) grid = a.ntiles;
   fn(a, dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "hiccl_reduce: launch");
@@ -760,7 +777,7 @@ int plan_kernel(hiccl_reduce_plan *p, uint32_t c0, uint64_t t0, uint64_t t1, int
                 hipStream_t s) {
   plan_fn fn = pick_plan(p->dtype, p->acc);
   if (!fn) return fail(hipErrorInvalidValue, "plan: unsupported dtype");
-  uint64_t grid = (uint64_t)device_cus(p->device) * 8;
+  uint64_t grid = (uint64_t)device_cus(p->device) * kPlanBpc;
   if (grid > t1 - t0) grid = t1 - t0;
   fn(p->d_desc, c0, t0, t1, dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "plan: launch");
@@ -791,7 +808,7 @@ int reduce_via_table(int dtype, int acc, void *out, const void *const *in, int n
                         "hiccl_reduce: table upload"))
     return e;
   plan_fn fn = pick_plan(dtype, acc);
-  uint64_t grid = (uint64_t)device_cus(current_device()) * 8;
+  uint64_t grid = (uint64_t)device_cus(current_device()) * kPlanBpc;
   if (grid > tiles) grid = tiles;
   fn((const PlanDesc *)dmem, 0, 0, tiles, dim3((unsigned)grid), s);
   if (int e = check_hip(hipGetLastError(), "hiccl_reduce: launch")) return e;
@@ -854,7 +871,7 @@ int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *p, void *stream) {
   if (int e = check_hip(hipSetDevice(p->device), "plan_launch: hipSetDevice")) return e;
   if (p->comps.empty()) return 0;
   if (int e = plan_upload(p)) return e;
-  hipStream_t s = stream ? (hipStream_t)stream : p->own;
+  hipStream_t s = (hipStream_t)stream;
   if (int e = plan_kernel(p, 0, 0, p->total_tiles, p->maxn, s)) return e;
   p->launched = true;
   return check_hip(hipEventRecord(p->done, s), "plan_launch: event");
@@ -865,7 +882,7 @@ int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *p, void *stream) {
   if (int e = check_hip(hipSetDevice(p->device), "plan_launch_each: hipSetDevice")) return e;
   if (p->comps.empty()) return 0;
   if (int e = plan_upload(p)) return e;
-  hipStream_t s = stream ? (hipStream_t)stream : p->own;
+  hipStream_t s = (hipStream_t)stream;
   for (size_t c = 0; c < p->comps.size(); c++) {
     const uint64_t t0 = p->host_desc[c].tile_begin;
     const uint64_t t1 = (c + 1 < p->comps.size()) ? p->host_desc[c + 1].tile_begin : p->total_tiles;
@@ -883,6 +900,8 @@ int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *p) {
 }
 
 int hiccl_reduce_plan_numcomp(const hiccl_reduce_plan_t *p) { return p ? (int)p->comps.size() : 0; }
+
+void *hiccl_reduce_plan_stream(const hiccl_reduce_plan_t *p) { return p ? (void *)p->own : nullptr; }
 
 size_t hiccl_reduce_plan_bytes(const hiccl_reduce_plan_t *p) {
   if (!p) return 0;

@@ -83,8 +83,10 @@ typedef struct {
   int block;         /* threads per workgroup: 256 or 512 */
   int unroll;        /* 16-byte packets per input per lane per tile: 1, 2 or 4 */
   int blocks_per_cu; /* persistent grid = CUs x this (capped by tiles) */
-  int nontemporal;   /* 0 plain, 1 nt loads, 2 nt loads + nt stores */
+  int nontemporal;   /* loads: 1 plain cache policy, 2 nt */
   int acc;           /* hiccl_acc_t */
+  int grid;          /* total workgroups; overrides blocks_per_cu when > 0 */
+  int store_policy;  /* stores: 1 plain, 2 nt, 3 sc1 (write-through, line dropped from L2) */
 } hiccl_reduce_config_t;
 
 int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t count,
@@ -102,8 +104,11 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
  *            pointers, copied.  (The reference's SPMD "only if myid ==
  *            compid" filter is applied by the C++ caller.)
  *   launch   compute.h:141-160 start(): one batched kernel on `stream`
- *            (NULL = the plan's own stream).  The first launch after an add
- *            uploads the descriptor table (synchronous, once).
+ *            (NULL = the default stream, as everywhere in this ABI; the
+ *            plan's own stream -- the reference creates one per compute,
+ *            compute.h:131-132 -- is hiccl_reduce_plan_stream()).  The first
+ *            launch after an add uploads the descriptor table (synchronous,
+ *            once).
  *   sync     compute.h:161-171 wait(): blocks until the plan's last launch
  *            has completed.
  *   destroy  frees the plan's device tables and stream (the reference leaks
@@ -123,6 +128,8 @@ int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *plan, void *stream);
  * the given stream (compute.h:141-145 launches one kernel per compute). */
 int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *plan, void *stream);
 int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *plan);
+/* The plan's own non-blocking stream (a hipStream_t), created with the plan. */
+void *hiccl_reduce_plan_stream(const hiccl_reduce_plan_t *plan);
 int hiccl_reduce_plan_numcomp(const hiccl_reduce_plan_t *plan);
 /* Sum over computes of count * (n + 1) * sizeof(T): the bytes the reference's
  * measure(warmup, numiter) overload (compute.h:251-257) prices. */

@@ -116,8 +116,10 @@ def test_tile_boundaries(oracle, count):
 @pytest.mark.parametrize("config", [
     dict(block=256, unroll=1), dict(block=256, unroll=2), dict(block=256, unroll=4),
     dict(block=512, unroll=1), dict(block=512, unroll=2), dict(block=512, unroll=4),
-    dict(block=256, unroll=2, nontemporal=1), dict(block=256, unroll=2, nontemporal=2),
-    dict(block=512, unroll=4, nontemporal=2, blocks_per_cu=2)])
+    dict(block=256, unroll=2, nontemporal=1), dict(block=256, unroll=2, nontemporal=2, store_policy=2),
+    dict(block=256, unroll=4, nontemporal=1, store_policy=3, grid=192),
+    dict(block=512, unroll=4, nontemporal=2, store_policy=2, blocks_per_cu=2),
+    dict(block=256, unroll=1, grid=7)])
 def test_tuning_variants_same_bits(oracle, config):
     for n, count in ((8, 1 << 20), (3, 123457)):
         x = oracle.fill(n, count, seed=n)
@@ -258,3 +260,30 @@ def test_full_size_sampled(oracle):
     idx2 = np.arange(0, count, stride * 1024, dtype=np.int64)
     got2 = out[torch.from_numpy(idx2).to(DEV)].cpu().numpy()
     assert bits_equal(got2, oracle.sample_sum(idx2.astype(np.uint64), seed, n))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.uint16])
+def test_plan_partitioned_on_default_stream(oracle, dtype):
+    """Config-4 layout: one bucket split into pipedepth computes with the
+    partition() formula (reduce.h:401-415: count/numbatch + (b < count%numbatch)),
+    launched as ONE batched kernel on torch's (NULL) default stream."""
+    n, count, depth = 8, 3 * 65536 + 1234, 7
+    tdt = TORCH_OF[np.dtype(dtype)]
+    x = oracle.fill(n, count, seed=21, dtype=dtype)
+    ins = [to_dev(r).view(tdt) for r in x]
+    out = torch.full((count,), 7.0, dtype=tdt, device=DEV)
+    comp = hiccl_amd.Compute(tdt, device=0)
+    off = 0
+    for b in range(depth):
+        c = count // depth + (1 if b < count % depth else 0)
+        comp.add([(t, off) for t in ins], (out, off), c, compid=0)
+        off += c
+    assert off == count
+    for each in (False, True):
+        out.fill_(7.0)
+        comp.start(stream=torch.cuda.current_stream(), each=each)
+        torch.cuda.synchronize()
+        got = to_host(out, dtype)
+        exp = oracle.reduce(list(x), dtype=dtype)
+        assert bits_equal(got, exp), (each, first_mismatch(got, exp))
+    comp.close()
