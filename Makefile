@@ -7,7 +7,7 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -Wall
 
 LIB = hiccl_amd/libhiccl_reduce.so
 
-all: $(LIB) oracle
+all: $(LIB) oracle cpp
 
 $(LIB): hiccl_amd/csrc/reduce.hip include/hiccl_reduce.h
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
@@ -20,3 +20,39 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# ---- C++ surface (include/hiccl.h): drivers and test tools -----------------
+MPI_INC ?= /opt/conda/include
+MPI_LIB ?= /opt/conda/lib
+CXX ?= g++
+CXXFLAGS = -std=c++17 -O2 -Wall -Wno-unused-function -Iinclude -I$(MPI_INC)
+MPI_LINK = $(MPI_LIB)/libmpi.so -Wl,-rpath,/usr/lib/x86_64-linux-gnu:$(MPI_LIB)
+HIP_HOST = -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
+HIP_LINK = -Lhiccl_amd -lhiccl_reduce -Wl,-rpath,'$$ORIGIN/../hiccl_amd' -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+HDRS = include/hiccl.h $(wildcard include/hiccl/*.h) include/hiccl_reduce.h hiccl_amd/csrc/compose.h
+
+CPP_BINS = build/plan_dump build/collectives_host build/collectives_host_f32 build/collectives_hip build/collectives_hip_f32
+
+cpp: $(CPP_BINS)
+
+build/plan_dump: tests/cpp/plan_dump.cpp $(HDRS)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -o $@ $< $(MPI_LINK)
+
+build/collectives_host: hiccl_amd/csrc/collectives.cpp $(HDRS)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -fopenmp -DHICCL_PORT_HOST -o $@ $< $(MPI_LINK)
+
+build/collectives_host_f32: hiccl_amd/csrc/collectives.cpp $(HDRS)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -fopenmp -DHICCL_PORT_HOST -DHICCL_DRIVER_FLOAT -o $@ $< $(MPI_LINK)
+
+build/collectives_hip: hiccl_amd/csrc/collectives.cpp $(HDRS) $(LIB)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) $(HIP_HOST) -o $@ $< $(HIP_LINK) $(MPI_LINK)
+
+build/collectives_hip_f32: hiccl_amd/csrc/collectives.cpp $(HDRS) $(LIB)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) $(HIP_HOST) -DHICCL_DRIVER_FLOAT -o $@ $< $(HIP_LINK) $(MPI_LINK)
+
+.PHONY: cpp

@@ -1,0 +1,149 @@
+// hiccl_amd/csrc/collectives.cpp -- this build's counterpart of the
+// reference driver collectives/main.cpp: compose one of the eight
+// collectives from HiCCL primitives, init, measure per command and whole
+// collective, validate with the known-answer test.
+//
+//   mpirun -np P build/collectives_{hip,host} pattern count numstripe ringnodes
+//          pipedepth warmup numiter [hierarchy libs] [dump_prefix]
+//
+//   pattern   1 gather .. 8 allreduce (hiccl.h:41)
+//   count     elements per rank per chunk (collectives/main.cpp:48)
+//   hierarchy comma list, e.g. 1,4,2 (default: numproc)      -- set_hierarchy
+//   libs      comma list of ipc|ipc_get|mpi|xccl per level    (default mpi)
+//   dump_prefix  if given, float inputs from the counter hash are used and
+//             every rank writes <prefix>.rank<r>.bin (its recvbuf) so tests
+//             can compare the exact bits with oracle/schedule.py.
+//
+// Element type: size_t (as the reference driver, collectives/main.cpp:24) or
+// float with -DHICCL_DRIVER_FLOAT.
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "compose.h"
+
+#ifdef HICCL_DRIVER_FLOAT
+typedef float Type;
+#else
+typedef size_t Type;
+#endif
+
+static std::vector<int> parse_ints(const char *s) {
+  std::vector<int> v;
+  std::string t(s);
+  size_t p = 0;
+  while (p <= t.size()) {
+    size_t q = t.find(',', p);
+    if (q == std::string::npos) q = t.size();
+    if (q > p) v.push_back(std::atoi(t.substr(p, q - p).c_str()));
+    p = q + 1;
+  }
+  return v;
+}
+
+static std::vector<CommBench::library> parse_libs(const char *s) {
+  std::vector<CommBench::library> v;
+  std::string t(s);
+  size_t p = 0;
+  while (p <= t.size()) {
+    size_t q = t.find(',', p);
+    if (q == std::string::npos) q = t.size();
+    std::string w = t.substr(p, q - p);
+    if (w == "ipc") v.push_back(CommBench::IPC);
+    else if (w == "ipc_get") v.push_back(CommBench::IPC_get);
+    else if (w == "mpi") v.push_back(CommBench::MPI);
+    else if (w == "xccl") v.push_back(CommBench::XCCL);
+    else if (!w.empty()) CommBench::die("driver", "unknown library " + w);
+    p = q + 1;
+  }
+  return v;
+}
+
+// oracle/reduce_oracle.c's generator (uniform [-1,1) of hash(seed, k, i)).
+static inline uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+static inline float uniform_f32(uint64_t seed, uint32_t k, uint64_t i) {
+  uint64_t h = splitmix64(splitmix64(seed ^ ((uint64_t)k << 48)) + i);
+  return (float)(uint32_t)(h >> 40) * (1.0f / 8388608.0f) - 1.0f;
+}
+
+int main(int argc, char *argv[]) {
+  CommBench::init();
+  const int myid = CommBench::myid, numproc = CommBench::numproc;
+  if (argc < 8) {
+    if (myid == 0)
+      std::fprintf(stderr, "usage: %s pattern count numstripe ringnodes pipedepth warmup numiter [hierarchy libs] [dump]\n",
+                   argv[0]);
+    MPI_Finalize();
+    return 2;
+  }
+  const int pattern = std::atoi(argv[1]);
+  const size_t count = std::atol(argv[2]);
+  const int numstripe = std::atoi(argv[3]), ringnodes = std::atoi(argv[4]), pipedepth = std::atoi(argv[5]);
+  const int warmup = std::atoi(argv[6]), numiter = std::atoi(argv[7]);
+  std::vector<int> hierarchy = {numproc};
+  std::vector<CommBench::library> libs = {CommBench::MPI};
+  if (argc > 9) {
+    hierarchy = parse_ints(argv[8]);
+    libs = parse_libs(argv[9]);
+  }
+  const char *dump = argc > 10 ? argv[10] : nullptr;
+  const int root = 0;
+
+  if (myid == 0) {
+    std::printf("\nNumber of processes: %d\nPattern: %d  count %zu (", numproc, pattern, count);
+    CommBench::print_data(count * sizeof(Type));
+    std::printf(")  numstripe %d ringnodes %d pipedepth %d\n", numstripe, ringnodes, pipedepth);
+  }
+
+  Type *sendbuf_d = nullptr, *recvbuf_d = nullptr;
+  CommBench::allocate(sendbuf_d, count * numproc);
+  CommBench::allocate(recvbuf_d, count * numproc);
+
+  int rc = 0;
+  {
+    HiCCL::Comm<Type> coll;
+    hiccl_driver::CommSink<Type> sink{coll};
+    if (!hiccl_driver::compose(sink, pattern, sendbuf_d, recvbuf_d, count, numproc, root)) {
+      if (myid == 0) std::printf("invalid collective option\n");
+      MPI_Finalize();
+      return 2;
+    }
+    coll.set_hierarchy(hierarchy, libs);
+    coll.set_numstripe(numstripe);
+    coll.set_ringnodes(ringnodes);
+    coll.set_pipedepth(pipedepth);
+    coll.init();
+    coll.report();
+
+    if (dump) {  // exact-bits run on float inputs from the counter hash
+      std::vector<Type> in(count * numproc);
+      for (size_t i = 0; i < in.size(); i++) in[i] = (Type)uniform_f32(1234, (uint32_t)myid, i);
+      CommBench::memcpyH2D(sendbuf_d, in.data(), in.size());
+      std::vector<Type> nanfill(count * numproc, (Type)-1);
+      CommBench::memcpyH2D(recvbuf_d, nanfill.data(), nanfill.size());
+      MPI_Barrier(CommBench::comm_mpi);
+      coll.run();
+      std::vector<Type> out(count * numproc);
+      CommBench::memcpyD2H(out.data(), recvbuf_d, out.size());
+      std::string path = std::string(dump) + ".rank" + std::to_string(myid) + ".bin";
+      FILE *f = std::fopen(path.c_str(), "wb");
+      if (!f || std::fwrite(out.data(), sizeof(Type), out.size(), f) != out.size()) CommBench::die("dump", path);
+      std::fclose(f);
+    }
+    if (numiter > 0) {
+      coll.measure(warmup, numiter, count * numproc / pipedepth);
+      HiCCL::measure<Type>(warmup, numiter, count * numproc, coll);
+    }
+    if (!dump || sizeof(Type) == 8) rc = HiCCL::validate(sendbuf_d, recvbuf_d, count, pattern, root, coll) ? 0 : 1;
+  }
+  CommBench::free(sendbuf_d);
+  CommBench::free(recvbuf_d);
+  MPI_Finalize();
+  return rc;
+}

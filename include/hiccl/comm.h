@@ -1,0 +1,321 @@
+// include/hiccl/comm.h -- HiCCL::Comm<T>, the persistent communicator
+// (reference: source/comm.h, source/init.h).
+//
+// Epochs of REDUCE/BROADCAST primitives separated by fences; init() turns
+// them into a pipeline of steps (init.h:2-76 + command.h implement);
+// run() executes it (comm.h:181-206): every library's transport starts, then
+// in reverse library order each transport completes and that library's
+// compute is launched, then every compute completes.
+//
+// Schedule<T> is the pure part (primitives + parameters -> merged steps for
+// one rank), so the factorization can be produced for any rank of any
+// machine size without MPI (tests/cpp/plan_dump.cpp).
+#ifndef HICCL_COMM_H
+#define HICCL_COMM_H
+
+#include <pthread.h>
+
+#include <cstdio>
+#include <list>
+#include <vector>
+
+#include "command.h"
+#include "compute.h"
+#include "plan.h"
+
+namespace HiCCL {
+
+enum pattern { all, others };
+
+template <typename T>
+struct Schedule {
+  std::vector<std::vector<BROADCAST<T>>> bcast_epoch;
+  std::vector<std::vector<REDUCE<T>>> reduce_epoch;
+  std::vector<int> hierarchy;
+  std::vector<CommBench::library> library;
+  int numstripe = 1, ringnodes = 1, pipedepth = 1;
+
+  void fence() {
+    bcast_epoch.emplace_back();
+    reduce_epoch.emplace_back();
+  }
+  void reduce(T *sb, size_t so, T *rb, size_t ro, size_t count, std::vector<int> ids, int recvid) {
+    reduce_epoch.back().emplace_back(sb, so, rb, ro, count, std::move(ids), recvid);
+  }
+  void bcast(T *sb, size_t so, T *rb, size_t ro, size_t count, int sendid, std::vector<int> ids) {
+    bcast_epoch.back().emplace_back(sb, so, rb, ro, count, sendid, std::move(ids));
+  }
+
+  // comm.h:160-179: groupsize[L-1] = h[L-1], groupsize[i] = groupsize[i+1]*h[i],
+  // then groupsize[0] = numproc / ringnodes.
+  std::vector<int> groupsizes(int np) const {
+    const int L = (int)hierarchy.size();
+    std::vector<int> g(L);
+    g[L - 1] = hierarchy[L - 1];
+    for (int i = L - 2; i >= 0; i--) g[i] = g[i + 1] * hierarchy[i];
+    g[0] = np / ringnodes;
+    return g;
+  }
+
+  // init.h:2-76 for rank `me` of `np`: per epoch, multicasts then
+  // reductions, each split into pipedepth batches; returns the per-batch
+  // level lists (coll_batch) and the planner's memory counters.
+  std::vector<CollList<T>> factorize(Planner<T> &P) const {
+    const int np = P.np, L = (int)hierarchy.size();
+    std::vector<int> gs = groupsizes(np), gt = gs;
+    gt[0] = np;
+    std::vector<CollList<T>> batches(pipedepth);
+    for (size_t e = 0; e < reduce_epoch.size(); e++) {
+      if (!bcast_epoch[e].empty()) {
+        auto parts = partition(bcast_epoch[e], pipedepth);
+        for (int b = 0; b < pipedepth; b++) {
+          auto split = P.stripe(numstripe, parts[b]);
+          typename Planner<T>::Pool pool;
+          P.reduce_tree(1, gt.data(), &library[L - 1], split, 0, batches[b], pool);
+          std::vector<BROADCAST<T>> intra;
+          P.bcast_ring(gs[0], library[0], parts[b], intra, batches[b]);
+          P.bcast_tree(L, gt.data(), library.data(), intra, 1, batches[b]);
+        }
+      }
+      if (!reduce_epoch[e].empty()) {
+        auto parts = partition(reduce_epoch[e], pipedepth);
+        for (int b = 0; b < pipedepth; b++) {
+          auto merge = P.stripe(numstripe, parts[b]);
+          std::vector<REDUCE<T>> intra;
+          P.reduce_ring(L, gs.data(), library.data(), parts[b], intra, batches[b]);
+          P.bcast_tree(L, gt.data(), library.data(), merge, 1, batches[b]);
+        }
+      }
+    }
+    return batches;
+  }
+};
+
+template <typename T>
+class Comm {
+ public:
+  // PIPELINE (comm.h:154-156): one list of commands per library
+  std::vector<std::list<Command<T>>> command_batch;
+  std::vector<CollList<T>> coll_batch;
+  std::vector<CommBench::library> libs;
+
+  Comm() {
+    sch.hierarchy = {CommBench::numproc};
+    sch.library = {CommBench::MPI};
+    add_fence();  // epoch 0 (comm.h:120-128)
+  }
+
+  // ------------------------------------------------------------ setters --
+  void set_hierarchy(std::vector<int> hierarchy, std::vector<CommBench::library> library) {
+    if (hierarchy.size() != library.size() || hierarchy.empty()) {
+      if (CommBench::myid == CommBench::printid) std::printf("hierarchy and library must have the same size!\n");
+      return;
+    }
+    sch.hierarchy = hierarchy;
+    sch.library = library;
+  }
+  void set_pipedepth(int d) { sch.pipedepth = d < 1 ? 1 : d; }
+  void set_numstripe(int s) { sch.numstripe = s < 1 ? 1 : s; }
+  void set_ringnodes(int r) { sch.ringnodes = r < 1 ? 1 : r; }
+  void set_endpoints(T *sb, size_t sc, T *rb, size_t rc) {
+    sendbuf = sb;
+    sendcount = sc;
+    recvbuf = rb;
+    recvcount = rc;
+  }
+
+  void print_parameters() const {
+    if (CommBench::myid != CommBench::printid) return;
+    std::printf("**************** HiCCL PARAMETERS\n%zu-level hierarchy:\n", sch.hierarchy.size());
+    for (size_t i = 0; i < sch.hierarchy.size(); i++)
+      std::printf("  level %zu factor: %d library: %s\n", i, sch.hierarchy[i], CommBench::lib_name(sch.library[i]));
+    std::printf("numstripe: %d\nringnodes: %d\npipedepth: %d\n", sch.numstripe, sch.ringnodes, sch.pipedepth);
+    std::printf("sendbuf: %p, sendcount %zu\nrecvbuf: %p, recvcount %zu\n", (void *)sendbuf, sendcount,
+                (void *)recvbuf, recvcount);
+    std::printf("*********************************\n");
+  }
+
+  // ------------------------------------------------------- primitives ----
+  void add_fence() {
+    sch.fence();
+    numepoch++;
+  }
+
+  // comm.h:131-143 (add_bcast) -- recvids as a list, a rank, or a pattern
+  void add_bcast(T *sb, size_t so, T *rb, size_t ro, size_t count, int sendid, std::vector<int> &recvids) {
+    sch.bcast(sb, so, rb, ro, count, sendid, recvids);
+  }
+  void add_bcast(T *sb, size_t so, T *rb, size_t ro, size_t count, int sendid, int recvid) {
+    sch.bcast(sb, so, rb, ro, count, sendid, expand_ids(recvid, CommBench::numproc, sendid));
+  }
+  void add_bcast(T *sb, size_t so, T *rb, size_t ro, size_t count, int sendid, pattern p) {
+    add_bcast(sb, so, rb, ro, count, sendid, p == others ? -1 : CommBench::numproc);
+  }
+
+  // comm.h:144-156 (add_reduce) -- sendids as a list, a rank, or a pattern
+  void add_reduce(T *sb, size_t so, T *rb, size_t ro, size_t count, std::vector<int> &sendids, int recvid) {
+    sch.reduce(sb, so, rb, ro, count, sendids, recvid);
+  }
+  void add_reduce(T *sb, size_t so, T *rb, size_t ro, size_t count, int sendid, int recvid) {
+    sch.reduce(sb, so, rb, ro, count, expand_ids(sendid, CommBench::numproc, recvid), recvid);
+  }
+  void add_reduce(T *sb, size_t so, T *rb, size_t ro, size_t count, pattern p, int recvid) {
+    add_reduce(sb, so, rb, ro, count, p == others ? -1 : CommBench::numproc, recvid);
+  }
+
+  // README.md:33,38 spellings (offset 0).
+  void add_reduction(T *sb, T *rb, size_t count, pattern p, int recvid) { add_reduce(sb, 0, rb, 0, count, p, recvid); }
+  void add_reduction(T *sb, T *rb, size_t count, int sendid, int recvid) { add_reduce(sb, 0, rb, 0, count, sendid, recvid); }
+  void add_reduction(T *sb, T *rb, size_t count, std::vector<int> &sendids, int recvid) {
+    add_reduce(sb, 0, rb, 0, count, sendids, recvid);
+  }
+  void add_multicast(T *sb, T *rb, size_t count, int sendid, pattern p) { add_bcast(sb, 0, rb, 0, count, sendid, p); }
+  void add_multicast(T *sb, T *rb, size_t count, int sendid, int recvid) { add_bcast(sb, 0, rb, 0, count, sendid, recvid); }
+  void add_multicast(T *sb, T *rb, size_t count, int sendid, std::vector<int> &recvids) {
+    add_bcast(sb, 0, rb, 0, count, sendid, recvids);
+  }
+
+  // ---------------------------------------------------------------- init --
+  // README.md:48 spelling: init(hierarchy, lib, numstripe, ring, pipeline)
+  void init(std::vector<int> hierarchy, std::vector<CommBench::library> lib, int numstripe, int ring, int pipeline) {
+    set_hierarchy(hierarchy, lib);
+    set_numstripe(numstripe);
+    set_ringnodes(ring);
+    set_pipedepth(pipeline);
+    init();
+  }
+
+  void init() {
+    if (CommBench::myid == CommBench::printid) print_parameters();
+    MPI_Barrier(CommBench::comm_mpi);
+    const double t0 = MPI_Wtime();
+    Planner<T> P(CommBench::myid, CommBench::numproc, [](size_t n) {
+      T *p = nullptr;
+      CommBench::allocate(p, n);
+      return p;
+    });
+    coll_batch = sch.factorize(P);
+    libs = libraries_used(coll_batch);
+    steps = merge_steps(coll_batch, libs, 1);
+    command_batch = instantiate(steps, libs);
+    buffsize = P.buffsize;
+    recycle = P.recycle;
+    reuse = P.reuse;
+    MPI_Barrier(CommBench::comm_mpi);  // nobody runs before every rank's handles are exchanged
+    report_memory();
+    if (CommBench::myid == CommBench::printid)
+      std::printf("initialization time: %e seconds (%zu steps, %zu libraries)\n", MPI_Wtime() - t0, steps.size(),
+                  libs.size());
+  }
+
+  // ----------------------------------------------------------------- run --
+  // comm.h:181-206
+  void run() {
+    const size_t nl = command_batch.size();
+    std::vector<typename std::list<Command<T>>::iterator> it(nl);
+    for (size_t i = 0; i < nl; i++) it[i] = command_batch[i].begin();
+    if (nl == 0) return;
+    while (it[0] != command_batch[0].end()) {  // every library has one command per step
+      for (size_t i = 0; i < nl; i++) it[i]->comm->start();
+      for (size_t i = nl; i-- > 0;) {
+        it[i]->comm->wait();
+        it[i]->compute->start();
+      }
+      for (size_t i = 0; i < nl; i++) {
+        it[i]->compute->wait();
+        ++it[i];
+      }
+    }
+  }
+
+  // comm.h:208-212
+  void run(T *sb, T *rb) {
+    CommBench::memcpyD2D(sendbuf, sb, sendcount);
+    run();
+    CommBench::memcpyD2D(rb, recvbuf, recvcount);
+  }
+
+  // comm.h:214-227: nonblocking run on a pthread bound to the rank's device.
+  void start() {
+    if (pthread_create(&thread, nullptr, &Comm<T>::run_async, this) != 0)
+      CommBench::die("Comm::start", "pthread_create failed");
+    running = true;
+  }
+  void wait() {
+    if (running) pthread_join(thread, nullptr);
+    running = false;
+  }
+
+  // comm.h:229-271: measure every command of the pipeline in step order.
+  void measure(int warmup, int numiter, size_t count) {
+    if (CommBench::myid == CommBench::printid)
+      std::printf("command_batch size %zu\ncommandlist size %zu\n", command_batch.size(),
+                  command_batch.empty() ? (size_t)0 : command_batch[0].size());
+    MPI_Barrier(CommBench::comm_mpi);
+    const size_t nl = command_batch.size();
+    if (!nl) return;
+    std::vector<typename std::list<Command<T>>::iterator> it(nl);
+    for (size_t i = 0; i < nl; i++) it[i] = command_batch[i].begin();
+    while (it[0] != command_batch[0].end()) {
+      if (CommBench::myid == CommBench::printid) std::printf("******************** MEASURE COMMANDS ********************\n");
+      for (size_t i = 0; i < nl; i++) {
+        it[i]->measure(warmup, numiter, count);
+        ++it[i];
+      }
+    }
+  }
+
+  // Per-step structure (the reference's report_pipeline, coll.h:97-152).
+  void report() const {
+    if (CommBench::myid != CommBench::printid) return;
+    std::printf("pipeline: %zu steps x %zu libraries\n", steps.size(), libs.size());
+    for (size_t s = 0; s < steps.size(); s++) {
+      std::printf("step %zu:\n", s);
+      for (auto &c : steps[s])
+        if (!c.empty()) {
+          std::printf("  ");
+          c.report(CommBench::numproc);
+        }
+    }
+  }
+
+  size_t numsteps() const { return steps.size(); }
+  const std::vector<std::vector<Coll<T>>> &plan() const { return steps; }
+  const Schedule<T> &schedule() const { return sch; }
+
+  size_t buffsize = 0, recycle = 0, reuse = 0;
+
+ private:
+  Schedule<T> sch;
+  int numepoch = 0;
+  T *sendbuf = nullptr, *recvbuf = nullptr;
+  size_t sendcount = 0, recvcount = 0;
+  std::vector<std::vector<Coll<T>>> steps;
+  pthread_t thread{};
+  bool running = false;
+
+  static void *run_async(void *arg) {
+    CommBench::setup_gpu();
+    static_cast<Comm<T> *>(arg)->run();
+    return nullptr;
+  }
+
+  // command.h:46-78 memory report
+  void report_memory() {
+    long v[3] = {(long)(buffsize * sizeof(T)), (long)(recycle * sizeof(T)), (long)(reuse * sizeof(T))};
+    MPI_Allreduce(MPI_IN_PLACE, v, 3, MPI_LONG, MPI_SUM, CommBench::comm_mpi);
+    if (CommBench::myid == CommBench::printid) {
+      std::printf("total buffsize: ");
+      CommBench::print_data(v[0]);
+      std::printf(" reuse: ");
+      CommBench::print_data(v[2]);
+      std::printf(" recycle: ");
+      CommBench::print_data(v[1]);
+      std::printf("\n");
+    }
+  }
+};
+
+}  // namespace HiCCL
+
+#endif  // HICCL_COMM_H

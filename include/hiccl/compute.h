@@ -1,0 +1,183 @@
+// include/hiccl/compute.h -- HiCCL::Compute<T>, the reduction compute stage.
+//
+// Same object contract as the reference (source/compute.h:80-258): add()
+// registers one compute on its owning rank (SPMD filter, compute.h:120),
+// start() launches every registered compute, wait() blocks until they are
+// done, report()/measure() print the reference's tables.  The MI355X port
+// keeps all registered computes in ONE hiccl_reduce_plan and start() is a
+// single batched kernel launch on the plan's stream (the reference launches
+// one reduce_kernel per compute on its own stream, compute.h:141-160, and
+// synchronises each, compute.h:161-171).
+//
+// Host port (HICCL_PORT_HOST, no GPU: config 1) runs the same in-order sum
+// with OpenMP on host memory, like the reference's no-PORT build
+// (compute.h:14-23).  It is selected at compile time; a HIP build contains no
+// CPU reduction.
+#ifndef HICCL_COMPUTE_H
+#define HICCL_COMPUTE_H
+
+#include <algorithm>
+#include <cstdio>
+#include <type_traits>
+#include <vector>
+
+#include "transport.h"
+
+#ifndef HICCL_PORT_HOST
+#include "../hiccl_reduce.h"
+#endif
+
+namespace HiCCL {
+
+// T -> hiccl_dtype_t
+template <typename T>
+constexpr int dtype_of() {
+  if constexpr (std::is_same<T, float>::value) return 0;
+  else if constexpr (std::is_same<T, double>::value) return 1;
+  else if constexpr (std::is_integral<T>::value && sizeof(T) == 8) return 3;
+  else if constexpr (std::is_integral<T>::value && sizeof(T) == 4) return 4;
+  else if constexpr (sizeof(T) == 2) return 2;  // bf16 storage type
+  else return -1;
+}
+
+template <typename T>
+class Compute {
+ public:
+  int numcomp = 0;
+  std::vector<std::vector<T *>> inputbuf;
+  std::vector<T *> outputbuf;
+  std::vector<size_t> count;
+
+  Compute() {}
+  ~Compute() {
+#ifndef HICCL_PORT_HOST
+    if (plan) hiccl_reduce_plan_destroy(plan);
+#endif
+  }
+  Compute(const Compute &) = delete;
+  Compute &operator=(const Compute &) = delete;
+
+  // compute.h:101-139.  Every rank calls add; the owning rank records.
+  void add(std::vector<T *> &in, T *out, size_t n, int compid) {
+    if (CommBench::myid != compid) return;
+    inputbuf.push_back(in);
+    outputbuf.push_back(out);
+    count.push_back(n);
+    numcomp++;
+#ifndef HICCL_PORT_HOST
+    static_assert(dtype_of<T>() >= 0, "HiCCL::Compute: unsupported element type");
+    if (!plan) check(hiccl_reduce_plan_create(&plan, dtype_of<T>(), CommBench::mydevice), "plan_create");
+    check(hiccl_reduce_plan_add(plan, out, (const void *const *)in.data(), (int)in.size(), n), "plan_add");
+#endif
+  }
+
+  // compute.h:141-160: nonblocking launch of all registered computes.
+  void start() {
+    if (!numcomp) return;
+#ifndef HICCL_PORT_HOST
+    check(hiccl_reduce_plan_launch(plan, hiccl_reduce_plan_stream(plan)), "plan_launch");
+#else
+    for (int c = 0; c < numcomp; c++) host_sum(outputbuf[c], count[c], inputbuf[c]);
+#endif
+  }
+
+  // compute.h:161-171
+  void wait() {
+#ifndef HICCL_PORT_HOST
+    if (numcomp) check(hiccl_reduce_plan_sync(plan), "plan_sync");
+#endif
+  }
+
+  // compute.h:173-189
+  void report() {
+    std::vector<int> nc(CommBench::numproc), ni(CommBench::numproc);
+    int numinput = 0;
+    for (auto &v : inputbuf) numinput += (int)v.size();
+    MPI_Allgather(&numcomp, 1, MPI_INT, nc.data(), 1, MPI_INT, CommBench::comm_mpi);
+    MPI_Allgather(&numinput, 1, MPI_INT, ni.data(), 1, MPI_INT, CommBench::comm_mpi);
+    if (CommBench::myid == CommBench::printid) {
+      std::printf("numcomp: ");
+      for (int p = 0; p < CommBench::numproc; p++) std::printf("%d(%d) ", nc[p], ni[p]);
+      std::printf("\n\n");
+    }
+  }
+
+  // compute.h:191-250: time start()+wait() with barriers, MAX over ranks,
+  // price `count` elements (the caller's choice, as the reference does).
+  void measure(int warmup, int numiter, size_t cnt) {
+    report();
+    std::vector<double> times;
+    if (CommBench::myid == CommBench::printid) {
+      std::printf("Measure Reduction Kernel\n%d warmup iterations (in order)\n", warmup);
+    }
+    for (int it = -warmup; it < numiter; it++) {
+#ifndef HICCL_PORT_HOST
+      CommBench::hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+#endif
+      MPI_Barrier(CommBench::comm_mpi);
+      double t0 = MPI_Wtime();
+      start();
+      double st = MPI_Wtime() - t0;
+      wait();
+      double t = MPI_Wtime() - t0;
+      MPI_Allreduce(MPI_IN_PLACE, &st, 1, MPI_DOUBLE, MPI_MAX, CommBench::comm_mpi);
+      MPI_Allreduce(MPI_IN_PLACE, &t, 1, MPI_DOUBLE, MPI_MAX, CommBench::comm_mpi);
+      if (it < 0) {
+        if (CommBench::myid == CommBench::printid) std::printf("startup %.2e warmup: %e\n", st, t);
+      } else {
+        times.push_back(t);
+      }
+    }
+    print_times(times, (double)cnt * sizeof(T));
+  }
+
+  // compute.h:251-257: price reads + writes, sum over ranks.
+  void measure(int warmup, int numiter) {
+    size_t tot = 0;
+    for (int c = 0; c < numcomp; c++) tot += count[c] * (inputbuf[c].size() + 1);
+    MPI_Allreduce(MPI_IN_PLACE, &tot, 1, MPI_UNSIGNED_LONG, MPI_SUM, CommBench::comm_mpi);
+    measure(warmup, numiter, tot);
+  }
+
+  static void print_times(std::vector<double> &times, double data) {
+    if (times.empty() || CommBench::myid != CommBench::printid) return;
+    std::sort(times.begin(), times.end());
+    const int n = (int)times.size();
+    std::printf("%d measurement iterations (sorted):\n", n);
+    for (int i = 0; i < n; i++)
+      std::printf("time: %.4e%s\n", times[i], i == 0 ? " -> min" : i == n / 2 ? " -> median" : i == n - 1 ? " -> max" : "");
+    double avg = 0;
+    for (double t : times) avg += t;
+    avg /= n;
+    std::printf("\ndata: ");
+    CommBench::print_data((size_t)data);
+    std::printf("\n");
+    const double v[4] = {times[0], times[n / 2], times[n - 1], avg};
+    const char *name[4] = {"min", "med", "max", "avg"};
+    for (int i = 0; i < 4; i++)
+      std::printf("%sTime: %.4e us, %.4e ms/GB, %.4e GB/s\n", name[i], v[i] * 1e6, v[i] / data * 1e12, data / v[i] / 1e9);
+    std::printf("\n");
+  }
+
+ private:
+#ifndef HICCL_PORT_HOST
+  hiccl_reduce_plan_t *plan = nullptr;
+  static void check(int e, const char *what) {
+    if (e) CommBench::die(what, hiccl_last_error());
+  }
+#else
+  static void host_sum(T *out, size_t n, const std::vector<T *> &in) {
+    const int k = (int)in.size();
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < n; i++) {
+      T acc = 0;
+      for (int j = 0; j < k; j++) acc += in[j][i];
+      out[i] = acc;
+    }
+  }
+#endif
+};
+
+}  // namespace HiCCL
+
+#endif  // HICCL_COMPUTE_H

@@ -1,0 +1,451 @@
+// include/hiccl/transport.h -- point-to-point transport under HiCCL's schedule.
+//
+// The reference builds on the CommBench submodule, which is not vendored
+// (/root/reference/.gitmodules:1-3, empty CommBench/).  This header provides
+// the names HiCCL and collectives/main.cpp call (call sites: SURVEY.md
+// section 1, L0 row) with an MI355X-native implementation:
+//
+//   control plane  MPI (rank/size, handle exchange, completion tokens)
+//   IPC / IPC_get  HIP IPC over xGMI: device allocations exported with
+//                  hipIpcGetMemHandle, opened once per peer allocation,
+//                  moved with hipMemcpyAsync by the writer (IPC, "put") or
+//                  the reader (IPC_get, "get"); ready/done tokens over MPI
+//                  keep a step from overwriting bytes a peer still reads
+//   MPI            MPI_Isend/Irecv; device buffers staged through pinned
+//                  host memory (MPICH here is not GPU-aware)
+//   XCCL           RCCL point-to-point when built with HICCL_WITH_RCCL,
+//                  otherwise served as IPC
+//   dummy          nothing
+//
+// Host port (HICCL_PORT_HOST, config 1: no GPU): buffers are host memory and
+// every library moves data with MPI.
+#ifndef HICCL_TRANSPORT_H
+#define HICCL_TRANSPORT_H
+
+#include <mpi.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#ifndef HICCL_PORT_HOST
+#include <hip/hip_runtime_api.h>
+#ifdef HICCL_WITH_RCCL
+#include <rccl/rccl.h>
+#endif
+#endif
+
+namespace CommBench {
+
+enum library { dummy, IPC, IPC_get, MPI, XCCL, numlib };
+
+inline MPI_Comm comm_mpi = MPI_COMM_NULL;
+inline int printid = 0;
+inline int myid = 0;
+inline int numproc = 1;
+inline int mydevice = 0;
+inline size_t memory = 0;  // bytes allocated through allocate()
+
+[[noreturn]] inline void die(const char *what, const std::string &msg) {
+  std::fprintf(stderr, "[hiccl rank %d] %s: %s\n", myid, what, msg.c_str());
+  std::fflush(stderr);
+  int init = 0;
+  MPI_Initialized(&init);
+  if (init) MPI_Abort(MPI_COMM_WORLD, 1);
+  std::abort();
+}
+
+#ifndef HICCL_PORT_HOST
+inline void hip_check(hipError_t e, const char *what) {
+  if (e != hipSuccess) die(what, hipGetErrorString(e));
+}
+#endif
+
+inline void mpi_check(int e, const char *what) {
+  if (e != MPI_SUCCESS) die(what, "MPI error " + std::to_string(e));
+}
+
+// Bind this thread to the rank's device (reference: setup_gpu before run()
+// on the Comm::start pthread, comm.h:214-216).
+inline void setup_gpu() {
+#ifndef HICCL_PORT_HOST
+  hip_check(hipSetDevice(mydevice), "hipSetDevice");
+#endif
+}
+
+// MPI bootstrap; one device per local rank (round-robin over visible GPUs).
+inline void init() {
+  int flag = 0;
+  MPI_Initialized(&flag);
+  if (!flag) {
+    int provided = 0;
+    MPI_Init_thread(nullptr, nullptr, MPI_THREAD_SERIALIZED, &provided);
+  }
+  if (comm_mpi == MPI_COMM_NULL) MPI_Comm_dup(MPI_COMM_WORLD, &comm_mpi);
+  MPI_Comm_rank(comm_mpi, &myid);
+  MPI_Comm_size(comm_mpi, &numproc);
+#ifndef HICCL_PORT_HOST
+  MPI_Comm local;
+  MPI_Comm_split_type(comm_mpi, MPI_COMM_TYPE_SHARED, myid, MPI_INFO_NULL, &local);
+  int lrank = 0;
+  MPI_Comm_rank(local, &lrank);
+  MPI_Comm_free(&local);
+  int ndev = 0;
+  hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+  if (ndev < 1) die("init", "no HIP device");
+  mydevice = lrank % ndev;
+  setup_gpu();
+#endif
+}
+
+inline void print_data(size_t bytes) {
+  if (bytes < 1e3) std::printf("%d bytes", (int)bytes);
+  else if (bytes < 1e6) std::printf("%.4f KB", bytes / 1e3);
+  else if (bytes < 1e9) std::printf("%.4f MB", bytes / 1e6);
+  else std::printf("%.4f GB", bytes / 1e9);
+}
+
+inline const char *lib_name(library lib) {
+  switch (lib) {
+    case dummy: return "dummy";
+    case IPC: return "IPC";
+    case IPC_get: return "IPC_get";
+    case MPI: return "MPI";
+    case XCCL: return "XCCL";
+    default: return "numlib";
+  }
+}
+
+inline void print_lib(library lib) { std::printf("%s", lib_name(lib)); }
+
+inline void report_memory() {
+  std::vector<size_t> all(numproc);
+  MPI_Allgather(&memory, sizeof(size_t), MPI_BYTE, all.data(), sizeof(size_t), MPI_BYTE, comm_mpi);
+  if (myid == printid) {
+    size_t tot = 0;
+    for (int p = 0; p < numproc; p++) tot += all[p];
+    std::printf("CommBench memory: ");
+    print_data(tot);
+    std::printf(" total over %d ranks\n", numproc);
+  }
+}
+
+// ------------------------------------------------------------- memory ----
+
+template <typename T>
+void allocate(T *&p, size_t n) {
+  const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+#ifdef HICCL_PORT_HOST
+  p = static_cast<T *>(std::malloc(bytes));
+  if (!p) die("allocate", "malloc failed");
+#else
+  hip_check(hipMalloc((void **)&p, bytes), "hipMalloc");
+#endif
+  memory += bytes;
+}
+
+template <typename T>
+void free(T *p) {
+  if (!p) return;
+#ifdef HICCL_PORT_HOST
+  std::free(p);
+#else
+  hip_check(hipFree(p), "hipFree");
+#endif
+}
+
+template <typename T>
+void memcpyH2D(T *d, const T *s, size_t n) {
+#ifdef HICCL_PORT_HOST
+  std::memcpy(d, s, n * sizeof(T));
+#else
+  hip_check(hipMemcpy(d, s, n * sizeof(T), hipMemcpyHostToDevice), "memcpyH2D");
+#endif
+}
+
+template <typename T>
+void memcpyD2H(T *d, const T *s, size_t n) {
+#ifdef HICCL_PORT_HOST
+  std::memcpy(d, s, n * sizeof(T));
+#else
+  hip_check(hipMemcpy(d, s, n * sizeof(T), hipMemcpyDeviceToHost), "memcpyD2H");
+#endif
+}
+
+template <typename T>
+void memcpyD2D(T *d, const T *s, size_t n) {
+#ifdef HICCL_PORT_HOST
+  std::memmove(d, s, n * sizeof(T));
+#else
+  hip_check(hipMemcpy(d, s, n * sizeof(T), hipMemcpyDeviceToDevice), "memcpyD2D");
+#endif
+}
+
+#ifndef HICCL_PORT_HOST
+// ------------------------------------------------------- IPC registry ----
+// One open mapping per (peer rank, peer allocation base).
+struct IpcKey {
+  int rank;
+  uintptr_t base;
+  bool operator<(const IpcKey &o) const { return rank != o.rank ? rank < o.rank : base < o.base; }
+};
+
+struct IpcExport {
+  hipIpcMemHandle_t handle;
+  uint64_t base;    // peer's allocation base (identifies the mapping)
+  uint64_t offset;  // byte offset of the buffer inside that allocation
+};
+
+inline std::map<IpcKey, char *> &ipc_opened() {
+  static std::map<IpcKey, char *> m;
+  return m;
+}
+
+inline IpcExport ipc_export(const void *p) {
+  IpcExport e;
+  std::memset(&e, 0, sizeof(e));
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  hip_check(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p), "hipMemGetAddressRange");
+  hip_check(hipIpcGetMemHandle(&e.handle, (void *)base), "hipIpcGetMemHandle");
+  e.base = (uint64_t)(uintptr_t)base;
+  e.offset = (uint64_t)((const char *)p - (const char *)base);
+  return e;
+}
+
+inline char *ipc_import(int peer, const IpcExport &e) {
+  IpcKey k{peer, (uintptr_t)e.base};
+  auto &m = ipc_opened();
+  auto it = m.find(k);
+  if (it == m.end()) {
+    void *ptr = nullptr;
+    hip_check(hipIpcOpenMemHandle(&ptr, e.handle, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    it = m.emplace(k, (char *)ptr).first;
+  }
+  return it->second + e.offset;
+}
+#endif
+
+// ------------------------------------------------------ point-to-point ----
+//
+// Comm<T>: a persistent set of registered transfers on one library,
+// SPMD-registered (every rank calls add for every transfer, in the same
+// order; only the two endpoints act), started and completed as a unit.
+// Call sites in the reference: command.h:122,132 (construction, add),
+// comm.h:190,197 (start, wait), command.h:17-37 (measure, numsend/numrecv).
+template <typename T>
+class Comm {
+ public:
+  library lib;
+  int numsend = 0;
+  int numrecv = 0;
+
+  explicit Comm(library lib) : lib(lib) {
+    if (this->lib == XCCL) {
+#if defined(HICCL_PORT_HOST) || !defined(HICCL_WITH_RCCL)
+      this->lib = IPC;  // served over the same xGMI path (see header comment)
+#endif
+    }
+#ifdef HICCL_PORT_HOST
+    if (this->lib != dummy) this->lib = MPI;
+#else
+    hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+#endif
+  }
+
+  ~Comm() {
+#ifndef HICCL_PORT_HOST
+    for (auto &x : xfers)
+      if (x.staging) (void)hipHostFree(x.staging);
+    if (stream) (void)hipStreamDestroy(stream);
+#endif
+  }
+
+  Comm(const Comm &) = delete;
+  Comm &operator=(const Comm &) = delete;
+
+  // Register one transfer: count elements from sendbuf+sendoffset on rank
+  // sendid to recvbuf+recvoffset on rank recvid.  Pointers need only be
+  // valid on their owning rank.
+  void add(T *sendbuf, size_t sendoffset, T *recvbuf, size_t recvoffset, size_t count, int sendid,
+           int recvid) {
+    Xfer x;
+    x.src = sendbuf ? sendbuf + sendoffset : nullptr;
+    x.dst = recvbuf ? recvbuf + recvoffset : nullptr;
+    x.count = count;
+    x.sendid = sendid;
+    x.recvid = recvid;
+    x.tag = (int)(xfers.size() % 30000);
+    if (myid == sendid) numsend++;
+    if (myid == recvid) numrecv++;
+    if (lib == dummy || count == 0) {
+      xfers.push_back(x);
+      return;
+    }
+    const bool me_send = myid == sendid, me_recv = myid == recvid;
+#ifndef HICCL_PORT_HOST
+    if (sendid != recvid && (lib == IPC || lib == IPC_get)) {
+      // the endpoint that moves the bytes needs the other side's mapping
+      const int exporter = lib == IPC ? recvid : sendid;
+      const int importer = lib == IPC ? sendid : recvid;
+      if (myid == exporter) {
+        IpcExport e = ipc_export(lib == IPC ? x.dst : x.src);
+        mpi_check(MPI_Send(&e, sizeof(e), MPI_BYTE, importer, x.tag, comm_mpi), "MPI_Send(ipc)");
+      }
+      if (myid == importer) {
+        IpcExport e;
+        mpi_check(MPI_Recv(&e, sizeof(e), MPI_BYTE, exporter, x.tag, comm_mpi, MPI_STATUS_IGNORE),
+                  "MPI_Recv(ipc)");
+        x.remote = ipc_import(exporter, e);
+      }
+    }
+    if (sendid != recvid && lib == MPI && (me_send || me_recv))
+      hip_check(hipHostMalloc((void **)&x.staging, count * sizeof(T), hipHostMallocDefault), "hipHostMalloc");
+#endif
+    (void)me_send;
+    (void)me_recv;
+    xfers.push_back(x);
+  }
+
+  void start() {
+    reqs.clear();
+    movers.clear();
+#ifndef HICCL_PORT_HOST
+    setup_gpu();
+#endif
+    for (auto &x : xfers) {
+      if (lib == dummy || x.count == 0) continue;
+      const bool me_send = myid == x.sendid, me_recv = myid == x.recvid;
+      if (!me_send && !me_recv) continue;
+      if (x.sendid == x.recvid) {  // self transfer
+#ifdef HICCL_PORT_HOST
+        std::memmove(x.dst, x.src, x.count * sizeof(T));
+#else
+        hip_check(hipMemcpyAsync(x.dst, x.src, x.count * sizeof(T), hipMemcpyDeviceToDevice, stream),
+                  "hipMemcpyAsync(self)");
+#endif
+        continue;
+      }
+      const int peer = me_send ? x.recvid : x.sendid;
+      if (lib == MPI) {
+#ifdef HICCL_PORT_HOST
+        post(me_send ? MPI_Isend(x.src, bytes(x), MPI_BYTE, peer, x.tag, comm_mpi, next())
+                     : MPI_Irecv(x.dst, bytes(x), MPI_BYTE, peer, x.tag, comm_mpi, next()));
+#else
+        if (me_send) {
+          hip_check(hipMemcpyAsync(x.staging, x.src, bytes(x), hipMemcpyDeviceToHost, stream), "stage D2H");
+          hip_check(hipStreamSynchronize(stream), "stage sync");
+          post(MPI_Isend(x.staging, bytes(x), MPI_BYTE, peer, x.tag, comm_mpi, next()));
+        } else {
+          post(MPI_Irecv(x.staging, bytes(x), MPI_BYTE, peer, x.tag, comm_mpi, next()));
+        }
+#endif
+        continue;
+      }
+#ifndef HICCL_PORT_HOST
+      // IPC / IPC_get: the mover waits for the owner's "ready" token, moves,
+      // then sends "done"; the owner posts "ready" now and waits for "done".
+      const bool mover = lib == IPC ? me_send : me_recv;
+      if (mover) {
+        movers.push_back({&x, (int)reqs.size()});
+        post(MPI_Irecv(nullptr, 0, MPI_BYTE, peer, x.tag, comm_mpi, next()));  // ready
+      } else {
+        post(MPI_Isend(nullptr, 0, MPI_BYTE, peer, x.tag, comm_mpi, next()));  // ready
+        post(MPI_Irecv(nullptr, 0, MPI_BYTE, peer, x.tag + 30000, comm_mpi, next()));  // done
+      }
+#endif
+    }
+  }
+
+  void wait() {
+#ifndef HICCL_PORT_HOST
+    setup_gpu();
+    for (auto &m : movers) {
+      mpi_check(MPI_Wait(&reqs[m.req], MPI_STATUS_IGNORE), "MPI_Wait(ready)");
+      Xfer &x = *m.x;
+      if (lib == IPC)
+        hip_check(hipMemcpyAsync(x.remote, x.src, bytes(x), hipMemcpyDeviceToDevice, stream), "IPC put");
+      else
+        hip_check(hipMemcpyAsync(x.dst, x.remote, bytes(x), hipMemcpyDeviceToDevice, stream), "IPC get");
+    }
+    hip_check(hipStreamSynchronize(stream), "transport stream sync");
+    for (auto &m : movers) {
+      const Xfer &x = *m.x;
+      const int peer = myid == x.sendid ? x.recvid : x.sendid;
+      post(MPI_Isend(nullptr, 0, MPI_BYTE, peer, x.tag + 30000, comm_mpi, next()));  // done
+    }
+#endif
+    if (!reqs.empty()) mpi_check(MPI_Waitall((int)reqs.size(), reqs.data(), MPI_STATUSES_IGNORE), "MPI_Waitall");
+    reqs.clear();
+#ifndef HICCL_PORT_HOST
+    if (lib == MPI) {  // unstage received bytes
+      for (auto &x : xfers)
+        if (myid == x.recvid && x.sendid != x.recvid && x.count)
+          hip_check(hipMemcpyAsync(x.dst, x.staging, bytes(x), hipMemcpyHostToDevice, stream), "unstage H2D");
+      hip_check(hipStreamSynchronize(stream), "unstage sync");
+    }
+#endif
+  }
+
+  // Per-step transport micro-benchmark (CommBench::Comm::measure call site:
+  // command.h:21).  Prints min/median/max like the reference's tables.
+  void measure(int warmup, int numiter, size_t count) {
+    std::vector<double> t;
+    for (int it = -warmup; it < numiter; it++) {
+      MPI_Barrier(comm_mpi);
+      double t0 = MPI_Wtime();
+      start();
+      wait();
+      double dt = MPI_Wtime() - t0;
+      MPI_Allreduce(MPI_IN_PLACE, &dt, 1, MPI_DOUBLE, MPI_MAX, comm_mpi);
+      if (it >= 0) t.push_back(dt);
+    }
+    std::sort(t.begin(), t.end());
+    if (myid == printid && !t.empty()) {
+      const double data = (double)count * sizeof(T);
+      std::printf("%s transfers: min %.4e s, median %.4e s, max %.4e s, %.3f GB/s (median)\n", lib_name(lib),
+                  t.front(), t[t.size() / 2], t.back(), data / t[t.size() / 2] / 1e9);
+    }
+  }
+
+  size_t size() const { return xfers.size(); }
+
+ private:
+  struct Xfer {
+    T *src = nullptr;
+    T *dst = nullptr;
+    char *remote = nullptr;  // peer mapping (IPC: peer's dst; IPC_get: peer's src)
+    T *staging = nullptr;    // pinned host staging (MPI with device memory)
+    size_t count = 0;
+    int sendid = 0, recvid = 0, tag = 0;
+  };
+  struct Mover {
+    Xfer *x;
+    int req;
+  };
+  std::vector<Xfer> xfers;
+  std::vector<MPI_Request> reqs;
+  std::vector<Mover> movers;
+#ifndef HICCL_PORT_HOST
+  hipStream_t stream = nullptr;
+#endif
+
+  static int bytes(const Xfer &x) {
+    const size_t b = x.count * sizeof(T);
+    if (b > (size_t)2147483647) die("transport", "message above 2 GiB: raise pipedepth");
+    return (int)b;
+  }
+  MPI_Request *next() {
+    reqs.emplace_back();
+    return &reqs.back();
+  }
+  static void post(int e) { mpi_check(e, "MPI post"); }
+};
+
+}  // namespace CommBench
+
+#endif  // HICCL_TRANSPORT_H
