@@ -1,0 +1,73 @@
+"""GPU tier: the C++ surface end to end on the HIP port.
+
+build/collectives_hip (hiccl_amd/csrc/collectives.cpp, default HIP port)
+under MPI with every rank on the box's GPU(s): HiCCL::Comm<T> factorizes,
+the transport moves device buffers (IPC put / IPC_get over HIP IPC handles,
+MPI with pinned staging), and each step's computes run as ONE batched
+gfx950 kernel through the C ABI.  At most 8 ranks touch the GPU.
+* the reference's known-answer test for all eight collectives (size_t);
+* float all-reduce: every rank's receive buffer equals oracle/schedule.py's
+  simulation of the reference schedule bit for bit.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import schedule as S  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+MPIRUN = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
+HIP = os.path.join(ROOT, "build", "collectives_hip")
+HIP_F32 = os.path.join(ROOT, "build", "collectives_hip_f32")
+
+
+def mpirun(np_, exe, args, timeout=180):
+    assert np_ <= 8
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = ["timeout", "-k", "10", str(timeout), MPIRUN, "-np", str(np_), exe] + [str(a) for a in args]
+    p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd="/tmp")
+    return p.returncode, p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("np_,hier,libs", [(2, "2", "ipc"), (4, "2,2", "mpi,ipc"), (4, "4", "ipc_get"),
+                                           (8, "1,4,2", "mpi,ipc,ipc")])
+@pytest.mark.parametrize("pattern", [4, 7, 8, 6, 1])
+def test_known_answer(np_, hier, libs, pattern):
+    rc, out = mpirun(np_, HIP, [pattern, 4099, 1, 1, 3, 0, 0, hier, libs])
+    assert rc == 0, out[-3000:]
+    assert "PASSED!" in out
+
+
+@pytest.mark.parametrize("np_,count,stripe,ring,depth,hier,libs", [
+    (2, 65536, 1, 1, 4, "2", "ipc"),
+    (4, 10007, 1, 1, 3, "2,2", "mpi,ipc"),
+    (8, 4099, 1, 1, 4, "1,4,2", "mpi,ipc,ipc"),
+    (8, 4099, 1, 2, 2, "2,4", "ipc,ipc_get"),
+])
+def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ring, depth, hier, libs):
+    prefix = str(tmp_path / "ar")
+    rc, out = mpirun(np_, HIP_F32, [8, count, stripe, ring, depth, 0, 0, hier, libs, prefix])
+    assert rc == 0, out[-3000:]
+    n = count * np_
+    x = {r: oracle.fill(r + 1, n, 1234)[r] for r in range(np_)}
+    libmap = {"mpi": S.MPI, "ipc": S.IPC, "ipc_get": S.IPC_GET, "xccl": S.XCCL}
+    sch = S.Schedule(np_, [int(h) for h in hier.split(",")], [libmap[lv] for lv in libs.split(",")],
+                     numstripe=stripe, ringnodes=ring, pipedepth=depth, ring_reuse_fix=True)
+    S.compose("allreduce", np_, count)(sch)
+    steps = sch.init()
+    user = {}
+    for r in range(np_):
+        user[(r, ("send",))] = x[r]
+        user[(r, ("recv",))] = np.full(n, -1.0, np.float32)
+    mem = S.simulate(steps, np_, user)
+    for r in range(np_):
+        got = np.fromfile(f"{prefix}.rank{r}.bin", dtype=np.float32)
+        exp = mem[(r, ("recv",))]
+        assert got.tobytes() == exp.tobytes(), f"rank {r}: {int((got != exp).sum())} differ"
