@@ -60,22 +60,37 @@ class Dist:
                 self.world = 1
             else:
                 log(f"bench: WORLD_SIZE={self.world} but --gpus {gpus}")
-        torch.cuda.set_device(self.local)
+        ndev = torch.cuda.device_count()
+        self.device = self.local % max(ndev, 1)
+        torch.cuda.set_device(self.device)
         self.pg = None
+        self.backend = None
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            # RCCL when every rank owns a GPU; gloo when ranks share one (a
+            # rehearsal on a 1-GPU box).  Either way only the barrier and the
+            # max-over-ranks time cross ranks: no data-path collective.
+            if self.world <= ndev:
+                self.backend = "nccl"
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.device))
+            else:
+                self.backend = "gloo"
+                dist.init_process_group("gloo")
             self.pg = dist
 
     def barrier(self):
         if self.pg:
-            self.pg.barrier(device_ids=[self.local])
+            if self.backend == "nccl":
+                self.pg.barrier(device_ids=[self.device])
+            else:
+                self.pg.barrier()
 
     def max(self, x):
         if not self.pg:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dev = "cuda" if self.backend == "nccl" else "cpu"
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
 
@@ -299,6 +314,7 @@ def main():
     del ins, out
     torch.cuda.empty_cache()
 
+    parity = bool(dist.max(0.0 if parity in (True, None) else 1.0) == 0.0) if parity is not None else None
     copy_gbps = copy_ceiling() if dist.rank == 0 else None
     prof = traffic_from_profiles(n, count)
     cpu = None
@@ -335,6 +351,7 @@ def main():
         "cpu_baseline": cpu,
         "parity_sample_ok": parity,
         "device": props.name,
+        "control_plane": dist.backend,
     }
     print(json.dumps(line), flush=True)
     return 0
