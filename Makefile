@@ -7,7 +7,12 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -fPIC -shared -std=c++17 -Wall
 
 LIB = hiccl_amd/libhiccl_reduce.so
 
-all: $(LIB) oracle cpp
+PROBE = tools/libhbm_probe.so
+
+all: $(LIB) $(PROBE) oracle cpp
+
+$(PROBE): tools/hbm_probe.hip
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
 $(LIB): hiccl_amd/csrc/reduce.hip include/hiccl_reduce.h
 	$(HIPCC) $(HIPFLAGS) -o $@ $<

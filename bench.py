@@ -133,6 +133,29 @@ def time_launches(fn, steps, warmup, dist=None):
     return t1 - t0, [a.elapsed_time(b) for a, b in evs]
 
 
+def mix_ceiling(ins, out, count, reps=10):
+    """Achievable HBM rate for this very access mix (n streams read + 1
+    written, 16 B/lane, XOR instead of add) from tools/libhbm_probe.so, at
+    the reduction kernel's geometry and at grid 192; None if not built."""
+    pso = os.path.join(ROOT, "tools", "libhbm_probe.so")
+    if not os.path.exists(pso):
+        return None
+    probe = ctypes.CDLL(pso)
+    probe.probe_run.restype = ctypes.c_int
+    probe.probe_run.argtypes = [ctypes.c_int] * 7 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                     ctypes.c_uint64, ctypes.c_void_p]
+    n = len(ins)
+    tab = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ins])
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    best = 0.0
+    for grid in (256, 192):
+        fn = lambda: probe.probe_run(0, 256, 4, 2, 2, 0, grid, tab, n, ctypes.c_void_p(out.data_ptr()),  # noqa: E731
+                                     count * 4, st)
+        _, ms = time_launches(fn, reps, 3)
+        best = max(best, (n + 1) * count * 4 / (np.median(ms) * 1e-3) / 1e9)
+    return best
+
+
 def copy_ceiling(nbytes=1 << 30, reps=10):
     src = torch.empty(nbytes // 4, device="cuda")
     dst = torch.empty_like(src)
@@ -311,6 +334,7 @@ def main():
         parity = bool(np.array_equal(got.view(np.uint32), exp.view(np.uint32)))
         if not parity:
             log("bench: PARITY FAILURE against the oracle sample")
+    mix_gbps = mix_ceiling(ins, out, count) if dist.rank == 0 else None
     del ins, out
     torch.cuda.empty_cache()
 
@@ -345,6 +369,8 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": (prof or {}).get("hbm_bytes_per_launch"),
                      "kernel_ms_mean": round(kern_s * 1e3, 4), "kernel_ms_min": round(min(kms), 4),
+                     "mix_ceiling_GBps": round(mix_gbps, 1) if mix_gbps else None,
+                     "frac_of_mix_ceiling": round(achieved / mix_gbps, 4) if mix_gbps else None,
                      "copy_ceiling_GBps": round(copy_gbps, 1) if copy_gbps else None,
                      "frac_of_copy": round(achieved / copy_gbps, 4) if copy_gbps else None,
                      "traffic_source": (prof or {}).get("source")},

@@ -831,12 +831,9 @@ int hiccl_reduce_plan_create(hiccl_reduce_plan_t **plan, int dtype, int device) 
   p->dtype = dtype;
   p->device = device;
   p->esz = esize(dtype);
-  if (int e = check_hip(hipStreamCreateWithFlags(&p->own, hipStreamNonBlocking), "plan_create: stream")) {
-    delete p;
-    return e;
-  }
+  // the plan's own stream is created on first request (hiccl_reduce_plan_stream):
+  // callers that launch on a shared stream never pay for one
   if (int e = check_hip(hipEventCreateWithFlags(&p->done, hipEventDisableTiming), "plan_create: event")) {
-    (void)hipStreamDestroy(p->own);
     delete p;
     return e;
   }
@@ -901,7 +898,14 @@ int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *p) {
 
 int hiccl_reduce_plan_numcomp(const hiccl_reduce_plan_t *p) { return p ? (int)p->comps.size() : 0; }
 
-void *hiccl_reduce_plan_stream(const hiccl_reduce_plan_t *p) { return p ? (void *)p->own : nullptr; }
+void *hiccl_reduce_plan_stream(hiccl_reduce_plan_t *p) {
+  if (!p) return nullptr;
+  if (!p->own) {
+    if (check_hip(hipSetDevice(p->device), "plan_stream: hipSetDevice")) return nullptr;
+    if (check_hip(hipStreamCreateWithFlags(&p->own, hipStreamNonBlocking), "plan_stream: create")) return nullptr;
+  }
+  return (void *)p->own;
+}
 
 size_t hiccl_reduce_plan_bytes(const hiccl_reduce_plan_t *p) {
   if (!p) return 0;

@@ -5,9 +5,9 @@
 // start() launches every registered compute, wait() blocks until they are
 // done, report()/measure() print the reference's tables.  The MI355X port
 // keeps all registered computes in ONE hiccl_reduce_plan and start() is a
-// single batched kernel launch on the plan's stream (the reference launches
-// one reduce_kernel per compute on its own stream, compute.h:141-160, and
-// synchronises each, compute.h:161-171).
+// single batched kernel launch on the process's compute stream (the
+// reference launches one reduce_kernel per compute on a stream of its own,
+// compute.h:141-160, and synchronises each, compute.h:161-171).
 //
 // Host port (HICCL_PORT_HOST, no GPU: config 1) runs the same in-order sum
 // with OpenMP on host memory, like the reference's no-PORT build
@@ -39,6 +39,18 @@ constexpr int dtype_of() {
   else if constexpr (sizeof(T) == 2) return 2;  // bf16 storage type
   else return -1;
 }
+
+#ifndef HICCL_PORT_HOST
+// One compute stream per process (see transport_stream()).
+inline hipStream_t compute_stream() {
+  static hipStream_t s = [] {
+    hipStream_t t;
+    CommBench::hip_check(hipStreamCreateWithFlags(&t, hipStreamNonBlocking), "hipStreamCreate(compute)");
+    return t;
+  }();
+  return s;
+}
+#endif
 
 template <typename T>
 class Compute {
@@ -75,7 +87,7 @@ class Compute {
   void start() {
     if (!numcomp) return;
 #ifndef HICCL_PORT_HOST
-    check(hiccl_reduce_plan_launch(plan, hiccl_reduce_plan_stream(plan)), "plan_launch");
+    check(hiccl_reduce_plan_launch(plan, compute_stream()), "plan_launch");
 #else
     for (int c = 0; c < numcomp; c++) host_sum(outputbuf[c], count[c], inputbuf[c]);
 #endif

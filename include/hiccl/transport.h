@@ -102,6 +102,20 @@ inline void init() {
 #endif
 }
 
+#ifndef HICCL_PORT_HOST
+// One transport stream per process: the steps of a pipeline run one after
+// the other on a rank, so every Comm shares it (the reference creates
+// streams per object; hundreds of them oversubscribe the hardware queues).
+inline hipStream_t transport_stream() {
+  static hipStream_t s = [] {
+    hipStream_t t;
+    hip_check(hipStreamCreateWithFlags(&t, hipStreamNonBlocking), "hipStreamCreate(transport)");
+    return t;
+  }();
+  return s;
+}
+#endif
+
 inline void print_data(size_t bytes) {
   if (bytes < 1e3) std::printf("%d bytes", (int)bytes);
   else if (bytes < 1e6) std::printf("%.4f KB", bytes / 1e3);
@@ -253,7 +267,7 @@ class Comm {
 #ifdef HICCL_PORT_HOST
     if (this->lib != dummy) this->lib = MPI;
 #else
-    hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+    stream = transport_stream();
 #endif
   }
 
@@ -261,7 +275,6 @@ class Comm {
 #ifndef HICCL_PORT_HOST
     for (auto &x : xfers)
       if (x.staging) (void)hipHostFree(x.staging);
-    if (stream) (void)hipStreamDestroy(stream);
 #endif
   }
 
@@ -314,6 +327,7 @@ class Comm {
   void start() {
     reqs.clear();
     movers.clear();
+    issued = false;
 #ifndef HICCL_PORT_HOST
     setup_gpu();
 #endif
@@ -327,6 +341,7 @@ class Comm {
 #else
         hip_check(hipMemcpyAsync(x.dst, x.src, x.count * sizeof(T), hipMemcpyDeviceToDevice, stream),
                   "hipMemcpyAsync(self)");
+        issued = true;
 #endif
         continue;
       }
@@ -372,7 +387,7 @@ class Comm {
       else
         hip_check(hipMemcpyAsync(x.dst, x.remote, bytes(x), hipMemcpyDeviceToDevice, stream), "IPC get");
     }
-    hip_check(hipStreamSynchronize(stream), "transport stream sync");
+    if (issued || !movers.empty()) hip_check(hipStreamSynchronize(stream), "transport stream sync");
     for (auto &m : movers) {
       const Xfer &x = *m.x;
       const int peer = myid == x.sendid ? x.recvid : x.sendid;
@@ -433,6 +448,7 @@ class Comm {
 #ifndef HICCL_PORT_HOST
   hipStream_t stream = nullptr;
 #endif
+  bool issued = false;  // async device work enqueued by start()
 
   static int bytes(const Xfer &x) {
     const size_t b = x.count * sizeof(T);

@@ -128,8 +128,9 @@ int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *plan, void *stream);
  * the given stream (compute.h:141-145 launches one kernel per compute). */
 int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *plan, void *stream);
 int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *plan);
-/* The plan's own non-blocking stream (a hipStream_t), created with the plan. */
-void *hiccl_reduce_plan_stream(const hiccl_reduce_plan_t *plan);
+/* The plan's own non-blocking stream (a hipStream_t), created on the first
+ * call and destroyed with the plan; NULL on error. */
+void *hiccl_reduce_plan_stream(hiccl_reduce_plan_t *plan);
 int hiccl_reduce_plan_numcomp(const hiccl_reduce_plan_t *plan);
 /* Sum over computes of count * (n + 1) * sizeof(T): the bytes the reference's
  * measure(warmup, numiter) overload (compute.h:251-257) prices. */
