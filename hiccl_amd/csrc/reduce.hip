@@ -432,6 +432,38 @@ __global__ void k_copy_bytes(char *dst, const char *src, uint64_t nbytes) {
   for (uint64_t i = threadIdx.x; i < nbytes; i += blockDim.x) dst[i] = src[i];
 }
 
+// ------------------------------------------------------ stream signalling --
+// One wave: lanes < nsig publish `epoch` to (typically peer, IPC-mapped)
+// flags with a system-scope release store; lanes < nwait spin on local flags
+// with system-scope acquire loads until they reach `epoch`.  Every spin is
+// bounded (s_memrealtime, 100 MHz): on timeout the lane records an error and
+// exits, so a broken protocol can never hang the GPU.
+
+constexpr int kMaxFlags = 64;
+
+struct SigWaitArgs {
+  uint32_t *sig[kMaxFlags];
+  const uint32_t *wait[kMaxFlags];
+  uint32_t *err;
+  uint64_t timeout_ticks;
+  uint32_t nsig, nwait, epoch, pad;
+};
+
+__global__ __launch_bounds__(64) void k_sigwait(SigWaitArgs a) {
+  const uint32_t lane = threadIdx.x;
+  if (lane < a.nsig) __hip_atomic_store(a.sig[lane], a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane < a.nwait) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int32_t)(__hip_atomic_load(a.wait[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+        if (a.err) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------ host side ----
 
 struct DevInfo {
@@ -923,6 +955,35 @@ void hiccl_reduce_plan_destroy(hiccl_reduce_plan_t *p) {
   if (p->done) (void)hipEventDestroy(p->done);
   if (p->own) (void)hipStreamDestroy(p->own);
   delete p;
+}
+
+// ---------------------------------------------------- stream signalling --
+
+int hiccl_signal_wait(uint32_t *const *sig, int nsig, const uint32_t *const *wait, int nwait,
+                      uint32_t epoch, uint32_t *err, double timeout_s, void *stream) {
+  if (nsig < 0 || nwait < 0 || (nsig && !sig) || (nwait && !wait))
+    return fail(hipErrorInvalidValue, "signal_wait: bad flag lists");
+  const uint64_t ticks = (uint64_t)((timeout_s > 0 ? timeout_s : 30.0) * 1e8);  // s_memrealtime: 100 MHz
+  hipStream_t s = (hipStream_t)stream;
+  int i = 0, j = 0;
+  while (i < nsig || j < nwait) {  // kMaxFlags of each per launch, in order
+    SigWaitArgs a;
+    memset(&a, 0, sizeof(a));
+    a.err = err;
+    a.timeout_ticks = ticks;
+    a.epoch = epoch;
+    for (; i < nsig && a.nsig < (uint32_t)kMaxFlags; i++) {
+      if (!sig[i]) return fail(hipErrorInvalidValue, "signal_wait: NULL signal flag");
+      a.sig[a.nsig++] = sig[i];
+    }
+    for (; j < nwait && a.nwait < (uint32_t)kMaxFlags; j++) {
+      if (!wait[j]) return fail(hipErrorInvalidValue, "signal_wait: NULL wait flag");
+      a.wait[a.nwait++] = wait[j];
+    }
+    hipLaunchKernelGGL(k_sigwait, dim3(1), dim3(64), 0, s, a);
+    if (int e = check_hip(hipGetLastError(), "signal_wait: launch")) return e;
+  }
+  return 0;
 }
 
 // ---------------------------------------------------------- measurement --

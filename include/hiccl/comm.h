@@ -16,7 +16,9 @@
 #include <pthread.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <list>
+#include <string>
 #include <vector>
 
 #include "command.h"
@@ -117,6 +119,11 @@ class Comm {
   void set_pipedepth(int d) { sch.pipedepth = d < 1 ? 1 : d; }
   void set_numstripe(int s) { sch.numstripe = s < 1 ? 1 : s; }
   void set_ringnodes(int r) { sch.ringnodes = r < 1 ? 1 : r; }
+  // Stream-ordered execution (HIP port, all ranks on one node): every step's
+  // transfers, their ready/done signalling and its compute are enqueued on
+  // the rank's stream and run() synchronises once at the end.  Default: on
+  // when HICCL_STREAM_ORDERED is unset or "1" and every rank shares a node.
+  void set_stream_ordered(bool on) { stream_req = on ? 1 : 0; }
   void set_endpoints(T *sb, size_t sc, T *rb, size_t rc) {
     sendbuf = sb;
     sendcount = sc;
@@ -197,20 +204,42 @@ class Comm {
     coll_batch = sch.factorize(P);
     libs = libraries_used(coll_batch);
     steps = merge_steps(coll_batch, libs, 1);
+    streamed = want_stream_mode();
+    CommBench::stream_ordered = streamed;
     command_batch = instantiate(steps, libs);
+    CommBench::stream_ordered = false;
+#ifndef HICCL_PORT_HOST
+    if (streamed) {  // one flag pair per registered transfer, every rank the same layout
+      size_t total = 0;
+      for (auto &lst : command_batch)
+        for (auto &c : lst) total += c.comm->size();
+      flags.create(2 * total);
+      size_t base = 0;
+      for (auto &lst : command_batch)
+        for (auto &c : lst) {
+          c.comm->bind(&flags, base);
+          base += c.comm->size();
+        }
+    }
+#endif
     buffsize = P.buffsize;
     recycle = P.recycle;
     reuse = P.reuse;
     MPI_Barrier(CommBench::comm_mpi);  // nobody runs before every rank's handles are exchanged
     report_memory();
     if (CommBench::myid == CommBench::printid)
-      std::printf("initialization time: %e seconds (%zu steps, %zu libraries)\n", MPI_Wtime() - t0, steps.size(),
-                  libs.size());
+      std::printf("initialization time: %e seconds (%zu steps, %zu libraries, %s)\n", MPI_Wtime() - t0, steps.size(),
+                  libs.size(), streamed ? "stream-ordered" : "host-driven");
   }
+
+  bool stream_ordered() const { return streamed; }
 
   // ----------------------------------------------------------------- run --
   // comm.h:181-206
   void run() {
+#ifndef HICCL_PORT_HOST
+    if (streamed) return run_streamed();
+#endif
     const size_t nl = command_batch.size();
     std::vector<typename std::list<Command<T>>::iterator> it(nl);
     for (size_t i = 0; i < nl; i++) it[i] = command_batch[i].begin();
@@ -293,6 +322,51 @@ class Comm {
   std::vector<std::vector<Coll<T>>> steps;
   pthread_t thread{};
   bool running = false;
+
+  int stream_req = -1;  // -1: decide from the environment and the node layout
+  bool streamed = false;
+#ifndef HICCL_PORT_HOST
+  CommBench::FlagSpace flags;
+
+  // Same order as run(), all of it enqueued on one stream: per step, every
+  // library's transport (ready signal, wait, copies, done signal, wait),
+  // then the computes in reverse library order; one synchronisation.
+  void run_streamed() {
+    CommBench::setup_gpu();
+    hipStream_t s = CommBench::transport_stream();
+    const size_t nl = command_batch.size();
+    std::vector<typename std::list<Command<T>>::iterator> it(nl);
+    for (size_t i = 0; i < nl; i++) it[i] = command_batch[i].begin();
+    if (nl == 0) return;
+    while (it[0] != command_batch[0].end()) {
+      for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
+      for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
+      for (size_t i = 0; i < nl; i++) ++it[i];
+    }
+    CommBench::hip_check(hipStreamSynchronize(s), "run: stream sync");
+    if (*flags.err) CommBench::die("run", "stream-ordered signal timed out (a peer never signalled)");
+  }
+#endif
+
+  bool want_stream_mode() {
+#ifdef HICCL_PORT_HOST
+    return false;
+#else
+    int on = stream_req;
+    if (on < 0) {
+      const char *env = std::getenv("HICCL_STREAM_ORDERED");
+      on = (!env || std::string(env) != "0") ? 1 : 0;
+    }
+    MPI_Comm local;
+    MPI_Comm_split_type(CommBench::comm_mpi, MPI_COMM_TYPE_SHARED, CommBench::myid, MPI_INFO_NULL, &local);
+    int lsize = 0;
+    MPI_Comm_size(local, &lsize);
+    MPI_Comm_free(&local);
+    int ok = on && lsize == CommBench::numproc;
+    MPI_Allreduce(MPI_IN_PLACE, &ok, 1, MPI_INT, MPI_LAND, CommBench::comm_mpi);
+    return ok != 0;
+#endif
+  }
 
   static void *run_async(void *arg) {
     CommBench::setup_gpu();

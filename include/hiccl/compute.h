@@ -93,6 +93,13 @@ class Compute {
 #endif
   }
 
+#ifndef HICCL_PORT_HOST
+  // Stream-ordered execution: enqueue the step's batched kernel on `s`.
+  void launch(hipStream_t s) {
+    if (numcomp) check(hiccl_reduce_plan_launch(plan, s), "plan_launch");
+  }
+#endif
+
   // compute.h:161-171
   void wait() {
 #ifndef HICCL_PORT_HOST

@@ -34,6 +34,8 @@
 
 #ifndef HICCL_PORT_HOST
 #include <hip/hip_runtime_api.h>
+
+#include "../hiccl_reduce.h"
 #ifdef HICCL_WITH_RCCL
 #include <rccl/rccl.h>
 #endif
@@ -49,6 +51,10 @@ inline int myid = 0;
 inline int numproc = 1;
 inline int mydevice = 0;
 inline size_t memory = 0;  // bytes allocated through allocate()
+// Stream-ordered mode (HIP port, every rank on one node): transfers and
+// their synchronisation are enqueued on the rank's stream, no host round
+// trip per step.  Set by HiCCL::Comm::init before it builds the transports.
+inline bool stream_ordered = false;
 
 [[noreturn]] inline void die(const char *what, const std::string &msg) {
   std::fprintf(stderr, "[hiccl rank %d] %s: %s\n", myid, what, msg.c_str());
@@ -242,7 +248,47 @@ inline char *ipc_import(int peer, const IpcExport &e) {
   }
   return it->second + e.offset;
 }
+
+// A communicator's flag array: one uint32 per slot in device memory on every
+// rank, IPC-mapped by every other rank (flags of peers are written remotely
+// with system-scope release stores, local flags polled with acquire loads by
+// hiccl_signal_wait).  err is host-visible and set by a timed-out spin.
+struct FlagSpace {
+  uint32_t *local = nullptr;
+  std::vector<uint32_t *> peer;  // peer[r]: rank r's array as mapped here (peer[myid] = local)
+  size_t nflags = 0;
+  uint32_t *err = nullptr;
+
+  // Collective over comm_mpi.
+  void create(size_t n) {
+    nflags = std::max<size_t>(n, 1);
+    hip_check(hipMalloc((void **)&local, nflags * sizeof(uint32_t)), "hipMalloc(flags)");
+    hip_check(hipMemset(local, 0, nflags * sizeof(uint32_t)), "hipMemset(flags)");
+    hip_check(hipHostMalloc((void **)&err, sizeof(uint32_t), hipHostMallocCoherent), "hipHostMalloc(err)");
+    *err = 0;
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize(flags)");
+    IpcExport mine = ipc_export(local);
+    std::vector<IpcExport> all(numproc);
+    mpi_check(MPI_Allgather(&mine, sizeof(IpcExport), MPI_BYTE, all.data(), sizeof(IpcExport), MPI_BYTE, comm_mpi),
+              "MPI_Allgather(flags)");
+    peer.assign(numproc, nullptr);
+    for (int r = 0; r < numproc; r++) peer[r] = r == myid ? local : (uint32_t *)ipc_import(r, all[r]);
+  }
+  ~FlagSpace() {
+    if (err) (void)hipHostFree(err);
+    if (local) (void)hipFree(local);
+  }
+};
+
+inline void signal_wait(const std::vector<uint32_t *> &sig, const std::vector<uint32_t *> &wait, uint32_t epoch,
+                        uint32_t *err, hipStream_t stream) {
+  if (sig.empty() && wait.empty()) return;
+  int e = hiccl_signal_wait(sig.data(), (int)sig.size(), (const uint32_t *const *)wait.data(), (int)wait.size(), epoch,
+                            err, 60.0, stream);
+  if (e) die("hiccl_signal_wait", hiccl_last_error());
+}
 #endif
+
 
 // ------------------------------------------------------ point-to-point ----
 //
@@ -251,6 +297,15 @@ inline char *ipc_import(int peer, const IpcExport &e) {
 // order; only the two endpoints act), started and completed as a unit.
 // Call sites in the reference: command.h:122,132 (construction, add),
 // comm.h:190,197 (start, wait), command.h:17-37 (measure, numsend/numrecv).
+//
+// Roles per transfer: the MOVER issues the copy (the sender for IPC "put",
+// the receiver for IPC_get), the OWNER is the other endpoint (it owns the
+// destination of a put / the source of a get).  Host-driven mode: the owner
+// posts a zero-byte "ready" to the mover at start(), the mover copies after
+// it and posts "done", the owner waits for "done" in wait().  Stream-ordered
+// mode: the same two signals are device flags (ready in the mover's
+// FlagSpace slot 2*(base+j), done in the owner's slot 2*(base+j)+1), set and
+// awaited by hiccl_signal_wait on the rank's stream around the copies.
 template <typename T>
 class Comm {
  public:
@@ -259,14 +314,12 @@ class Comm {
   int numrecv = 0;
 
   explicit Comm(library lib) : lib(lib) {
-    if (this->lib == XCCL) {
-#if defined(HICCL_PORT_HOST) || !defined(HICCL_WITH_RCCL)
-      this->lib = IPC;  // served over the same xGMI path (see header comment)
-#endif
-    }
 #ifdef HICCL_PORT_HOST
     if (this->lib != dummy) this->lib = MPI;
 #else
+    streamed = stream_ordered;
+    if (this->lib == XCCL) this->lib = IPC;  // served over the same xGMI path (see header comment)
+    if (streamed && this->lib == MPI) this->lib = IPC;  // one node: move device bytes directly
     stream = transport_stream();
 #endif
   }
@@ -299,38 +352,87 @@ class Comm {
       xfers.push_back(x);
       return;
     }
-    const bool me_send = myid == sendid, me_recv = myid == recvid;
 #ifndef HICCL_PORT_HOST
     if (sendid != recvid && (lib == IPC || lib == IPC_get)) {
-      // the endpoint that moves the bytes needs the other side's mapping
-      const int exporter = lib == IPC ? recvid : sendid;
-      const int importer = lib == IPC ? sendid : recvid;
-      if (myid == exporter) {
+      // the mover needs a mapping of the owner's buffer
+      const int owner = lib == IPC ? recvid : sendid;
+      const int mover = lib == IPC ? sendid : recvid;
+      if (myid == owner) {
         IpcExport e = ipc_export(lib == IPC ? x.dst : x.src);
-        mpi_check(MPI_Send(&e, sizeof(e), MPI_BYTE, importer, x.tag, comm_mpi), "MPI_Send(ipc)");
+        mpi_check(MPI_Send(&e, sizeof(e), MPI_BYTE, mover, x.tag, comm_mpi), "MPI_Send(ipc)");
       }
-      if (myid == importer) {
+      if (myid == mover) {
         IpcExport e;
-        mpi_check(MPI_Recv(&e, sizeof(e), MPI_BYTE, exporter, x.tag, comm_mpi, MPI_STATUS_IGNORE),
-                  "MPI_Recv(ipc)");
-        x.remote = ipc_import(exporter, e);
+        mpi_check(MPI_Recv(&e, sizeof(e), MPI_BYTE, owner, x.tag, comm_mpi, MPI_STATUS_IGNORE), "MPI_Recv(ipc)");
+        x.remote = ipc_import(owner, e);
       }
     }
-    if (sendid != recvid && lib == MPI && (me_send || me_recv))
+    if (sendid != recvid && lib == MPI && (myid == sendid || myid == recvid))
       hip_check(hipHostMalloc((void **)&x.staging, count * sizeof(T), hipHostMallocDefault), "hipHostMalloc");
 #endif
-    (void)me_send;
-    (void)me_recv;
     xfers.push_back(x);
   }
 
+#ifndef HICCL_PORT_HOST
+  // Stream-ordered mode: assign flag slots [2*base, 2*(base+size())) of fs.
+  void bind(FlagSpace *fs, size_t base) {
+    flags = fs;
+    pre_sig.clear();
+    pre_wait.clear();
+    post_sig.clear();
+    post_wait.clear();
+    moves.clear();
+    for (size_t j = 0; j < xfers.size(); j++) {
+      const Xfer &x = xfers[j];
+      if (lib == dummy || x.count == 0 || x.sendid == x.recvid) continue;
+      const int owner = lib == IPC ? x.recvid : x.sendid;
+      const int mover = lib == IPC ? x.sendid : x.recvid;
+      const size_t ready = 2 * (base + j), done = ready + 1;
+      if (myid == owner) {
+        pre_sig.push_back(fs->peer[mover] + ready);
+        post_wait.push_back(fs->local + done);
+      }
+      if (myid == mover) {
+        pre_wait.push_back(fs->local + ready);
+        post_sig.push_back(fs->peer[owner] + done);
+        moves.push_back(j);
+      }
+    }
+  }
+
+  // Enqueue one execution on `s` without waiting: owners signal ready,
+  // movers wait for ready, copy, signal done, owners wait for done.
+  void enqueue(hipStream_t s) {
+    ++epoch;
+    signal_wait(pre_sig, pre_wait, epoch, flags->err, s);
+    for (size_t j : moves) {
+      const Xfer &x = xfers[j];
+      if (lib == IPC)
+        hip_check(hipMemcpyAsync(x.remote, x.src, x.count * sizeof(T), hipMemcpyDeviceToDevice, s), "IPC put");
+      else
+        hip_check(hipMemcpyAsync(x.dst, x.remote, x.count * sizeof(T), hipMemcpyDeviceToDevice, s), "IPC get");
+    }
+    for (const Xfer &x : xfers)
+      if (lib != dummy && x.count && x.sendid == x.recvid && x.sendid == myid)
+        hip_check(hipMemcpyAsync(x.dst, x.src, x.count * sizeof(T), hipMemcpyDeviceToDevice, s), "self copy");
+    signal_wait(post_sig, post_wait, epoch, flags->err, s);
+  }
+
+  bool stream_mode() const { return streamed; }
+#endif
+
   void start() {
+#ifndef HICCL_PORT_HOST
+    setup_gpu();
+    if (streamed) {
+      if (!flags) die("transport", "stream-ordered Comm used before bind()");
+      enqueue(stream);
+      return;
+    }
+#endif
     reqs.clear();
     movers.clear();
     issued = false;
-#ifndef HICCL_PORT_HOST
-    setup_gpu();
-#endif
     for (auto &x : xfers) {
       if (lib == dummy || x.count == 0) continue;
       const bool me_send = myid == x.sendid, me_recv = myid == x.recvid;
@@ -362,8 +464,6 @@ class Comm {
         continue;
       }
 #ifndef HICCL_PORT_HOST
-      // IPC / IPC_get: the mover waits for the owner's "ready" token, moves,
-      // then sends "done"; the owner posts "ready" now and waits for "done".
       const bool mover = lib == IPC ? me_send : me_recv;
       if (mover) {
         movers.push_back({&x, (int)reqs.size()});
@@ -379,6 +479,11 @@ class Comm {
   void wait() {
 #ifndef HICCL_PORT_HOST
     setup_gpu();
+    if (streamed) {
+      hip_check(hipStreamSynchronize(stream), "transport stream sync");
+      if (flags && *flags->err) die("transport", "stream-ordered signal timed out (peer never signalled)");
+      return;
+    }
     for (auto &m : movers) {
       mpi_check(MPI_Wait(&reqs[m.req], MPI_STATUS_IGNORE), "MPI_Wait(ready)");
       Xfer &x = *m.x;
@@ -433,7 +538,7 @@ class Comm {
   struct Xfer {
     T *src = nullptr;
     T *dst = nullptr;
-    char *remote = nullptr;  // peer mapping (IPC: peer's dst; IPC_get: peer's src)
+    char *remote = nullptr;  // mapping of the owner's buffer (IPC: its dst; IPC_get: its src)
     T *staging = nullptr;    // pinned host staging (MPI with device memory)
     size_t count = 0;
     int sendid = 0, recvid = 0, tag = 0;
@@ -445,10 +550,15 @@ class Comm {
   std::vector<Xfer> xfers;
   std::vector<MPI_Request> reqs;
   std::vector<Mover> movers;
+  bool issued = false;  // async device work enqueued by start()
 #ifndef HICCL_PORT_HOST
   hipStream_t stream = nullptr;
+  bool streamed = false;
+  FlagSpace *flags = nullptr;
+  uint32_t epoch = 0;
+  std::vector<uint32_t *> pre_sig, pre_wait, post_sig, post_wait;
+  std::vector<size_t> moves;
 #endif
-  bool issued = false;  // async device work enqueued by start()
 
   static int bytes(const Xfer &x) {
     const size_t b = x.count * sizeof(T);

@@ -138,6 +138,21 @@ size_t hiccl_reduce_plan_bytes(const hiccl_reduce_plan_t *plan);
 void hiccl_reduce_plan_destroy(hiccl_reduce_plan_t *plan);
 
 /* ----------------------------------------------------------------------
+ * Stream-ordered signalling for the transport (include/hiccl/transport.h).
+ *
+ * Enqueues on `stream` (after all earlier work on it): a system-scope
+ * release store of `epoch` to each of the nsig flags `sig` (typically flags
+ * in a peer's IPC-mapped device memory), then a bounded spin until each of
+ * the nwait local flags `wait` holds a value >= epoch (32-bit wrap-aware),
+ * with system-scope acquire.  A spin exceeding timeout_s (<= 0: 30 s) stores
+ * 1 to *err (if err is not NULL; host-visible memory recommended) and gives
+ * up instead of hanging.  Replaces, per pipeline step, the host round trip
+ * the reference's transport makes around every transfer (comm.h:188-204).
+ */
+int hiccl_signal_wait(uint32_t *const *sig, int nsig, const uint32_t *const *wait, int nwait,
+                      uint32_t epoch, uint32_t *err, double timeout_s, void *stream);
+
+/* ----------------------------------------------------------------------
  * Measurement utilities (bench.py; not part of the reference surface).
  *
  * fill_uniform: element i of buffer k = uniform [-1,1) value of hash

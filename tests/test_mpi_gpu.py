@@ -28,21 +28,23 @@ HIP = os.path.join(ROOT, "build", "collectives_hip")
 HIP_F32 = os.path.join(ROOT, "build", "collectives_hip_f32")
 
 
-def mpirun(np_, exe, args, timeout=180):
+def mpirun(np_, exe, args, timeout=180, streamed=True):
     assert np_ <= 8
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED="1" if streamed else "0")
     cmd = ["timeout", "-k", "10", str(timeout), MPIRUN, "-np", str(np_), exe] + [str(a) for a in args]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd="/tmp")
     return p.returncode, p.stdout + p.stderr
 
 
+@pytest.mark.parametrize("streamed", [True, False], ids=["stream", "host"])
 @pytest.mark.parametrize("np_,hier,libs", [(2, "2", "ipc"), (4, "2,2", "mpi,ipc"), (4, "4", "ipc_get"),
                                            (8, "1,4,2", "mpi,ipc,ipc")])
 @pytest.mark.parametrize("pattern", [4, 7, 8, 6, 1])
-def test_known_answer(np_, hier, libs, pattern):
-    rc, out = mpirun(np_, HIP, [pattern, 4099, 1, 1, 3, 0, 0, hier, libs])
+def test_known_answer(np_, hier, libs, pattern, streamed):
+    rc, out = mpirun(np_, HIP, [pattern, 4099, 1, 1, 3, 0, 0, hier, libs], streamed=streamed)
     assert rc == 0, out[-3000:]
     assert "PASSED!" in out
+    assert ("stream-ordered" if streamed else "host-driven") in out
 
 
 @pytest.mark.parametrize("np_,count,stripe,ring,depth,hier,libs", [
@@ -51,9 +53,10 @@ def test_known_answer(np_, hier, libs, pattern):
     (8, 4099, 1, 1, 4, "1,4,2", "mpi,ipc,ipc"),
     (8, 4099, 1, 2, 2, "2,4", "ipc,ipc_get"),
 ])
-def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ring, depth, hier, libs):
+@pytest.mark.parametrize("streamed", [True, False], ids=["stream", "host"])
+def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ring, depth, hier, libs, streamed):
     prefix = str(tmp_path / "ar")
-    rc, out = mpirun(np_, HIP_F32, [8, count, stripe, ring, depth, 0, 0, hier, libs, prefix])
+    rc, out = mpirun(np_, HIP_F32, [8, count, stripe, ring, depth, 0, 0, hier, libs, prefix], streamed=streamed)
     assert rc == 0, out[-3000:]
     n = count * np_
     x = {r: oracle.fill(r + 1, n, 1234)[r] for r in range(np_)}
