@@ -23,6 +23,7 @@ HICCL_FLOAT64 = 1
 HICCL_BFLOAT16 = 2
 HICCL_UINT64 = 3
 HICCL_INT32 = 4
+HICCL_BYTES = 5
 
 HICCL_ACC_NATIVE = 0
 HICCL_ACC_WIDE = 1

@@ -221,6 +221,20 @@ struct OpBF16Wide {
   __device__ static void sstore(char *p, sacc_t a) { *(uint16_t *)p = bf_round(a); }
 };
 
+// Exact byte copy (HICCL_BYTES): one input, out = in[0] bit for bit.  The
+// transport's batched data movement runs on the same tile engine.
+struct OpRaw {
+  static constexpr int kEsz = 1;
+  typedef u32x4 acc_t;
+  __device__ static acc_t zero() { return (u32x4)(0u); }
+  __device__ static acc_t add(acc_t, u32x4 p) { return p; }
+  __device__ static u32x4 pack(acc_t a) { return a; }
+  typedef uint8_t sacc_t;
+  __device__ static sacc_t szero() { return 0; }
+  __device__ static sacc_t sadd(sacc_t, const char *p) { return *(const uint8_t *)p; }
+  __device__ static void sstore(char *p, sacc_t a) { *(uint8_t *)p = a; }
+};
+
 // ----------------------------------------------------------- tile engine --
 //
 // A compute is split as [head scalars | npkt 16-B packets | tail scalars],
@@ -456,6 +470,8 @@ __global__ __launch_bounds__(64) void k_sigwait(SigWaitArgs a) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while ((int32_t)(__hip_atomic_load(a.wait[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
       __builtin_amdgcn_s_sleep(2);
+      // an earlier timeout (any wait of this rank) ends every later spin at once
+      if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
       if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
         if (a.err) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -499,6 +515,7 @@ size_t esize(int dtype) {
     case HICCL_BFLOAT16: return 2;
     case HICCL_UINT64: return 8;
     case HICCL_INT32: return 4;
+    case HICCL_BYTES: return 1;
     default: return 0;
   }
 }
@@ -622,6 +639,7 @@ single_fn pick_single_dtype(int dtype, const Cfg &c) {
     case HICCL_FLOAT64: return pick_single<OpF64, false>(c);
     case HICCL_UINT64: return pick_single<OpU64, false>(c);
     case HICCL_INT32: return pick_single<OpI32, false>(c);
+    case HICCL_BYTES: return pick_single<OpRaw, false>(c);
     default: return nullptr;
   }
 }
@@ -649,6 +667,7 @@ plan_fn pick_plan(int dtype, int acc) {
     case HICCL_FLOAT64: return launch_plan_t<OpF64>;
     case HICCL_UINT64: return launch_plan_t<OpU64>;
     case HICCL_INT32: return launch_plan_t<OpI32>;
+    case HICCL_BYTES: return launch_plan_t<OpRaw>;
     default: return nullptr;
   }
 }
@@ -682,6 +701,7 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
   const size_t esz = esize(dtype);
   if (!esz) return fail(hipErrorInvalidValue, "hiccl_reduce: unknown dtype " + std::to_string(dtype));
   if (count == 0) return 0;
+  if (dtype == HICCL_BYTES && n != 1) return fail(hipErrorInvalidValue, "hiccl_reduce: HICCL_BYTES copies need n == 1");
   if (int e = check_buffers(out, in, n, count, esz)) return e;
   Cfg c = resolve(cfg);
   if (c.acc != HICCL_ACC_NATIVE && c.acc != HICCL_ACC_WIDE)
@@ -884,6 +904,7 @@ int hiccl_reduce_plan_set_acc(hiccl_reduce_plan_t *p, int acc) {
 int hiccl_reduce_plan_add(hiccl_reduce_plan_t *p, void *out, const void *const *in, int n,
                           size_t count) {
   if (!p) return fail(hipErrorInvalidValue, "plan_add: plan is NULL");
+  if (p->dtype == HICCL_BYTES && n != 1) return fail(hipErrorInvalidValue, "plan_add: HICCL_BYTES copies need n == 1");
   if (int e = check_buffers(out, in, n, count, p->esz)) return e;
   if (count == 0) return 0;
   hiccl_reduce_plan::Comp c;

@@ -121,8 +121,11 @@ class Comm {
   void set_ringnodes(int r) { sch.ringnodes = r < 1 ? 1 : r; }
   // Stream-ordered execution (HIP port, all ranks on one node): every step's
   // transfers, their ready/done signalling and its compute are enqueued on
-  // the rank's stream and run() synchronises once at the end.  Default: on
-  // when HICCL_STREAM_ORDERED is unset or "1" and every rank shares a node.
+  // the rank's stream and run() synchronises once at the end.  Opt-in
+  // (HICCL_STREAM_ORDERED=1 or this setter): on the single-GPU rehearsals we
+  // can run, ranks sharing one device serialise and the host-driven mode is
+  // faster; with one process per GPU this mode removes
+  // every host round trip per step.
   void set_stream_ordered(bool on) { stream_req = on ? 1 : 0; }
   void set_endpoints(T *sb, size_t sc, T *rb, size_t rc) {
     sendbuf = sb;
@@ -355,7 +358,7 @@ class Comm {
     int on = stream_req;
     if (on < 0) {
       const char *env = std::getenv("HICCL_STREAM_ORDERED");
-      on = (!env || std::string(env) != "0") ? 1 : 0;
+      on = (env && std::string(env) == "1") ? 1 : 0;
     }
     MPI_Comm local;
     MPI_Comm_split_type(CommBench::comm_mpi, MPI_COMM_TYPE_SHARED, CommBench::myid, MPI_INFO_NULL, &local);

@@ -280,11 +280,22 @@ struct FlagSpace {
   }
 };
 
+// Seconds a stream-ordered wait may spin before it reports a timeout
+// (HICCL_SIGNAL_TIMEOUT, default 60).
+inline double signal_timeout() {
+  static double t = [] {
+    const char *e = std::getenv("HICCL_SIGNAL_TIMEOUT");
+    double v = e ? std::atof(e) : 60.0;
+    return v > 0 ? v : 60.0;
+  }();
+  return t;
+}
+
 inline void signal_wait(const std::vector<uint32_t *> &sig, const std::vector<uint32_t *> &wait, uint32_t epoch,
                         uint32_t *err, hipStream_t stream) {
   if (sig.empty() && wait.empty()) return;
   int e = hiccl_signal_wait(sig.data(), (int)sig.size(), (const uint32_t *const *)wait.data(), (int)wait.size(), epoch,
-                            err, 60.0, stream);
+                            err, signal_timeout(), stream);
   if (e) die("hiccl_signal_wait", hiccl_last_error());
 }
 #endif
@@ -328,6 +339,8 @@ class Comm {
 #ifndef HICCL_PORT_HOST
     for (auto &x : xfers)
       if (x.staging) (void)hipHostFree(x.staging);
+    if (moveplan) hiccl_reduce_plan_destroy(moveplan);
+    if (selfplan) hiccl_reduce_plan_destroy(selfplan);
 #endif
   }
 
@@ -381,7 +394,6 @@ class Comm {
     pre_wait.clear();
     post_sig.clear();
     post_wait.clear();
-    moves.clear();
     for (size_t j = 0; j < xfers.size(); j++) {
       const Xfer &x = xfers[j];
       if (lib == dummy || x.count == 0 || x.sendid == x.recvid) continue;
@@ -395,7 +407,6 @@ class Comm {
       if (myid == mover) {
         pre_wait.push_back(fs->local + ready);
         post_sig.push_back(fs->peer[owner] + done);
-        moves.push_back(j);
       }
     }
   }
@@ -405,16 +416,7 @@ class Comm {
   void enqueue(hipStream_t s) {
     ++epoch;
     signal_wait(pre_sig, pre_wait, epoch, flags->err, s);
-    for (size_t j : moves) {
-      const Xfer &x = xfers[j];
-      if (lib == IPC)
-        hip_check(hipMemcpyAsync(x.remote, x.src, x.count * sizeof(T), hipMemcpyDeviceToDevice, s), "IPC put");
-      else
-        hip_check(hipMemcpyAsync(x.dst, x.remote, x.count * sizeof(T), hipMemcpyDeviceToDevice, s), "IPC get");
-    }
-    for (const Xfer &x : xfers)
-      if (lib != dummy && x.count && x.sendid == x.recvid && x.sendid == myid)
-        hip_check(hipMemcpyAsync(x.dst, x.src, x.count * sizeof(T), hipMemcpyDeviceToDevice, s), "self copy");
+    launch_copies(s);
     signal_wait(post_sig, post_wait, epoch, flags->err, s);
   }
 
@@ -429,21 +431,24 @@ class Comm {
       enqueue(stream);
       return;
     }
+    build_plans();
 #endif
     reqs.clear();
     movers.clear();
     issued = false;
+#ifndef HICCL_PORT_HOST
+    if (selfplan) {
+      launch_plan(selfplan, stream, "self copies");
+      issued = true;
+    }
+#endif
     for (auto &x : xfers) {
       if (lib == dummy || x.count == 0) continue;
       const bool me_send = myid == x.sendid, me_recv = myid == x.recvid;
       if (!me_send && !me_recv) continue;
-      if (x.sendid == x.recvid) {  // self transfer
+      if (x.sendid == x.recvid) {  // self transfer (device: in the batched self-copy below)
 #ifdef HICCL_PORT_HOST
         std::memmove(x.dst, x.src, x.count * sizeof(T));
-#else
-        hip_check(hipMemcpyAsync(x.dst, x.src, x.count * sizeof(T), hipMemcpyDeviceToDevice, stream),
-                  "hipMemcpyAsync(self)");
-        issued = true;
 #endif
         continue;
       }
@@ -484,14 +489,8 @@ class Comm {
       if (flags && *flags->err) die("transport", "stream-ordered signal timed out (peer never signalled)");
       return;
     }
-    for (auto &m : movers) {
-      mpi_check(MPI_Wait(&reqs[m.req], MPI_STATUS_IGNORE), "MPI_Wait(ready)");
-      Xfer &x = *m.x;
-      if (lib == IPC)
-        hip_check(hipMemcpyAsync(x.remote, x.src, bytes(x), hipMemcpyDeviceToDevice, stream), "IPC put");
-      else
-        hip_check(hipMemcpyAsync(x.dst, x.remote, bytes(x), hipMemcpyDeviceToDevice, stream), "IPC get");
-    }
+    for (auto &m : movers) mpi_check(MPI_Wait(&reqs[m.req], MPI_STATUS_IGNORE), "MPI_Wait(ready)");
+    if (!movers.empty() && moveplan) launch_plan(moveplan, stream, "IPC moves");  // every move, one kernel
     if (issued || !movers.empty()) hip_check(hipStreamSynchronize(stream), "transport stream sync");
     for (auto &m : movers) {
       const Xfer &x = *m.x;
@@ -557,7 +556,39 @@ class Comm {
   FlagSpace *flags = nullptr;
   uint32_t epoch = 0;
   std::vector<uint32_t *> pre_sig, pre_wait, post_sig, post_wait;
-  std::vector<size_t> moves;
+  // batched exact copies (HICCL_BYTES plans): the bytes this rank moves to or
+  // from peers, and its self transfers -- one kernel each per execution
+  hiccl_reduce_plan_t *moveplan = nullptr, *selfplan = nullptr;
+  bool planned = false;
+
+  void build_plans() {
+    if (planned) return;
+    planned = true;
+    if (lib == dummy) return;
+    for (const Xfer &x : xfers) {
+      if (!x.count) continue;
+      const bool self = x.sendid == x.recvid && x.sendid == myid;
+      const bool move = x.sendid != x.recvid && (lib == IPC || lib == IPC_get) &&
+                        myid == (lib == IPC ? x.sendid : x.recvid);
+      if (!self && !move) continue;
+      hiccl_reduce_plan_t *&p = self ? selfplan : moveplan;
+      if (!p && hiccl_reduce_plan_create(&p, HICCL_BYTES, mydevice)) die("transport", hiccl_last_error());
+      const void *src = self || lib == IPC ? (const void *)x.src : (const void *)x.remote;
+      void *dst = self || lib == IPC_get ? (void *)x.dst : (void *)x.remote;
+      if (lib == IPC && !self) dst = x.remote;
+      if (hiccl_reduce_plan_add(p, dst, &src, 1, x.count * sizeof(T))) die("transport copy plan", hiccl_last_error());
+    }
+  }
+
+  static void launch_plan(hiccl_reduce_plan_t *p, hipStream_t s, const char *what) {
+    if (hiccl_reduce_plan_launch(p, s)) die(what, hiccl_last_error());
+  }
+
+  void launch_copies(hipStream_t s) {
+    build_plans();
+    if (moveplan) launch_plan(moveplan, s, "IPC moves");
+    if (selfplan) launch_plan(selfplan, s, "self copies");
+  }
 #endif
 
   static int bytes(const Xfer &x) {

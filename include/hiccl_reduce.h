@@ -39,7 +39,8 @@ typedef enum {
   HICCL_BFLOAT16 = 2,
   HICCL_UINT64 = 3, /* size_t */
   HICCL_INT32 = 4,
-  HICCL_NUM_DTYPES = 5
+  HICCL_BYTES = 5,  /* exact copy, exactly one input: out = in[0] (transport data movement) */
+  HICCL_NUM_DTYPES = 6
 } hiccl_dtype_t;
 
 /* Accumulation mode (only meaningful for HICCL_BFLOAT16). */

@@ -33,7 +33,7 @@ def test_gfx950_code_object_embedded():
 
 def test_dtype_sizes_and_version():
     lib = L.lib()
-    assert [lib.hiccl_dtype_size(d) for d in range(5)] == [4, 8, 2, 8, 4]
+    assert [lib.hiccl_dtype_size(d) for d in range(6)] == [4, 8, 2, 8, 4, 1]
     assert lib.hiccl_dtype_size(99) == 0
     assert lib.hiccl_version() >= 100
 
@@ -62,6 +62,9 @@ def test_invalid_arguments_rejected_on_host():
     assert "overlaps" in L.last_error()
     # negative n
     assert lib.hiccl_reduce(0, ctypes.c_void_p(0x1000), _tab([]), -1, 4, None) == 1
+    # byte copies take exactly one input
+    assert lib.hiccl_reduce(5, ctypes.c_void_p(0x1000), _tab([0x2000, 0x3000]), 2, 4, None) == 1
+    assert "n == 1" in L.last_error()
     # unsupported tuning config
     cfg = L.ReduceConfig(block=128)
     assert lib.hiccl_reduce_ex(0, ctypes.c_void_p(0x1000), _tab([0x2000]), 1, 4, None, ctypes.byref(cfg)) == 1

@@ -30,7 +30,8 @@ HIP_F32 = os.path.join(ROOT, "build", "collectives_hip_f32")
 
 def mpirun(np_, exe, args, timeout=180, streamed=True):
     assert np_ <= 8
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED="1" if streamed else "0")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED="1" if streamed else "0",
+               HICCL_SIGNAL_TIMEOUT="10")
     cmd = ["timeout", "-k", "10", str(timeout), MPIRUN, "-np", str(np_), exe] + [str(a) for a in args]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd="/tmp")
     return p.returncode, p.stdout + p.stderr

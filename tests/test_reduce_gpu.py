@@ -287,3 +287,37 @@ def test_plan_partitioned_on_default_stream(oracle, dtype):
         exp = oracle.reduce(list(x), dtype=dtype)
         assert bits_equal(got, exp), (each, first_mismatch(got, exp))
     comp.close()
+
+
+@pytest.mark.parametrize("nbytes", [1, 15, 16, 17, 4099, 1 << 20, (1 << 22) + 7])
+def test_byte_copy_exact(nbytes):
+    """HICCL_BYTES: an exact copy (NaN payloads and -0 preserved), any byte
+    offsets, one launch for a batch of copies (the transport's data path)."""
+    rng = np.random.default_rng(nbytes)
+    src = torch.from_numpy(rng.integers(0, 256, nbytes + 64, dtype=np.uint8)).to(DEV)
+    import ctypes
+    from hiccl_amd import _lib as L
+    lib = L.lib()
+    plan = ctypes.c_void_p()
+    assert lib.hiccl_reduce_plan_create(ctypes.byref(plan), L.HICCL_BYTES, 0) == 0
+    outs = []
+    for so, do in ((0, 0), (1, 3), (5, 0), (13, 11)):
+        dst = torch.zeros(nbytes + 64, dtype=torch.uint8, device=DEV)
+        tab = (ctypes.c_void_p * 1)(src.data_ptr() + so)
+        assert lib.hiccl_reduce_plan_add(plan, ctypes.c_void_p(dst.data_ptr() + do), tab, 1, nbytes) == 0, L.last_error()
+        outs.append((dst, so, do))
+    assert lib.hiccl_reduce_plan_launch(plan, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+    torch.cuda.synchronize()
+    s = src.cpu().numpy()
+    for dst, so, do in outs:
+        d = dst.cpu().numpy()
+        assert np.array_equal(d[do:do + nbytes], s[so:so + nbytes])
+        assert not d[:do].any() and not d[do + nbytes:].any()
+    lib.hiccl_reduce_plan_destroy(plan)
+    # float payloads survive a byte copy bit for bit (no 0 + x)
+    f = torch.tensor([-0.0, float("nan"), 1.5, -2.25], device=DEV)
+    f.view(torch.int32)[1] = 0x7FA00001
+    g = torch.empty_like(f)
+    hiccl_amd.reduce_ptrs(L.HICCL_BYTES, g.data_ptr(), [f.data_ptr()], 16)
+    torch.cuda.synchronize()
+    assert g.view(torch.int32).tolist() == f.view(torch.int32).tolist()
