@@ -36,7 +36,8 @@ HIP_HOST = -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
 HIP_LINK = -Lhiccl_amd -lhiccl_reduce -Wl,-rpath,'$$ORIGIN/../hiccl_amd' -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
 HDRS = include/hiccl.h $(wildcard include/hiccl/*.h) include/hiccl_reduce.h hiccl_amd/csrc/compose.h
 
-CPP_BINS = build/plan_dump build/collectives_host build/collectives_host_f32 build/collectives_hip build/collectives_hip_f32
+CPP_BINS = build/plan_dump build/collectives_host build/collectives_host_f32 build/collectives_hip build/collectives_hip_f32 \
+           build/readme_example_host build/readme_example_hip
 
 cpp: $(CPP_BINS)
 
@@ -59,5 +60,13 @@ build/collectives_hip: hiccl_amd/csrc/collectives.cpp $(HDRS) $(LIB)
 build/collectives_hip_f32: hiccl_amd/csrc/collectives.cpp $(HDRS) $(LIB)
 	@mkdir -p build
 	$(CXX) $(CXXFLAGS) $(HIP_HOST) -DHICCL_DRIVER_FLOAT -o $@ $< $(HIP_LINK) $(MPI_LINK)
+
+build/readme_example_host: hiccl_amd/csrc/readme_example.cpp $(HDRS)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -fopenmp -DHICCL_PORT_HOST -o $@ $< $(MPI_LINK)
+
+build/readme_example_hip: hiccl_amd/csrc/readme_example.cpp $(HDRS) $(LIB)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) $(HIP_HOST) -o $@ $< $(HIP_LINK) $(MPI_LINK)
 
 .PHONY: cpp

@@ -22,6 +22,14 @@
 #ifndef HICCL_TRANSPORT_H
 #define HICCL_TRANSPORT_H
 
+// The deprecated MPI C++ bindings would declare a namespace MPI that
+// collides with the library name MPI used unqualified (README.md:46).
+#ifndef MPICH_SKIP_MPICXX
+#define MPICH_SKIP_MPICXX 1
+#endif
+#ifndef OMPI_SKIP_MPICXX
+#define OMPI_SKIP_MPICXX 1
+#endif
 #include <mpi.h>
 
 #include <algorithm>

@@ -75,3 +75,11 @@ def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ri
         got = np.fromfile(f"{prefix}.rank{r}.bin", dtype=np.float32)
         exp = mem[(r, ("recv",))]
         assert got.tobytes() == exp.tobytes(), f"rank {r}: {int((got != exp).sum())} differ"
+
+
+@pytest.mark.parametrize("streamed", [True, False], ids=["stream", "host"])
+@pytest.mark.parametrize("np_", [2, 4])
+def test_readme_api_example(np_, streamed):
+    rc, out = mpirun(np_, os.path.join(ROOT, "build", "readme_example_hip"), [250000, 3], streamed=streamed)
+    assert rc == 0, out[-3000:]
+    assert "README all-reduce: PASSED" in out

@@ -31,8 +31,8 @@ pytestmark = pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
 
 @pytest.fixture(scope="module", autouse=True)
 def built():
-    subprocess.run(["make", "-C", ROOT, "build/collectives_host", "build/collectives_host_f32"], check=True,
-                   stdout=subprocess.DEVNULL)
+    subprocess.run(["make", "-C", ROOT, "build/collectives_host", "build/collectives_host_f32",
+                    "build/readme_example_host"], check=True, stdout=subprocess.DEVNULL)
 
 
 def mpirun(np_, exe, args, timeout=240):
@@ -85,3 +85,12 @@ def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ri
         got = np.fromfile(f"{prefix}.rank{r}.bin", dtype=np.float32)
         exp = mem[(r, ("recv",))]
         assert got.tobytes() == exp.tobytes(), f"rank {r}: {int((got != exp).sum())} differ"
+
+
+@pytest.mark.parametrize("np_", [1, 2, 4, 6])
+def test_readme_api_example(np_):
+    """README.md:12-60 spellings: add_reduction / add_fence / add_multicast /
+    init(hierarchy, lib, numstripe, ring, pipeline) / start() / wait()."""
+    rc, out = mpirun(np_, os.path.join(ROOT, "build", "readme_example_host"), [1001, 3])
+    assert rc == 0, out
+    assert "README all-reduce: PASSED" in out
