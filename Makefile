@@ -9,7 +9,7 @@ LIB = hiccl_amd/libhiccl_reduce.so
 
 PROBE = tools/libhbm_probe.so
 
-all: $(LIB) $(PROBE) oracle cpp
+all: $(LIB) $(PROBE) cpp oracle
 
 $(PROBE): tools/hbm_probe.hip
 	$(HIPCC) $(HIPFLAGS) -o $@ $<

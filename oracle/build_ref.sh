@@ -36,3 +36,28 @@ grep -q 'void reduce_kernel' <<<"$FRAG" || { echo "build_ref: reduce_kernel not 
   echo 'extern "C" void ref_reduce_u64(size_t *o, size_t c, size_t **in, int n) { HiCCL::reduce_kernel<size_t>(o, c, in, n); }'
 } | g++ -x c++ -std=c++17 -O3 -fopenmp -fPIC -shared -o "$OUT" -
 echo "build_ref: built $OUT from $SRC"
+
+# ---------------------------------------------------------------------------
+# Drop-in check: the reference's OWN driver, collectives/main.cpp, compiled
+# unmodified against THIS build's include/hiccl.h.  The source is fed on
+# stdin from inside include/hiccl/, so its `#include "../hiccl.h"`
+# (collectives/main.cpp:17) resolves to include/hiccl.h; nothing is edited or
+# copied.  Host port (no GPU) and HIP port (gfx950 reduction library).
+DRV="$REF/collectives/main.cpp"
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUTDIR=$(cd "$(dirname "$OUT")" && pwd)
+MPI_INC=${MPI_INC:-/opt/conda/include}
+MPI_LIB=${MPI_LIB:-/opt/conda/lib}
+if [ -f "$DRV" ] && [ -f "$MPI_INC/mpi.h" ]; then
+  MPI_LINK="$MPI_LIB/libmpi.so -Wl,-rpath,/usr/lib/x86_64-linux-gnu:$MPI_LIB"
+  ( cd "$ROOT/include/hiccl" && g++ -std=c++17 -O2 -fopenmp -DHICCL_PORT_HOST -I"$MPI_INC" \
+      -x c++ - -x none -o "$OUTDIR/collectives_main_host" $MPI_LINK < "$DRV" )
+  echo "build_ref: built $OUTDIR/collectives_main_host from $DRV against include/hiccl.h"
+  if [ -f "$ROOT/hiccl_amd/libhiccl_reduce.so" ]; then
+    ( cd "$ROOT/include/hiccl" && g++ -std=c++17 -O2 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -I"$MPI_INC" \
+        -x c++ - -x none -o "$OUTDIR/collectives_main_hip" \
+        -L"$ROOT/hiccl_amd" -lhiccl_reduce -Wl,-rpath,'$ORIGIN/../../hiccl_amd' \
+        -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib $MPI_LINK < "$DRV" )
+    echo "build_ref: built $OUTDIR/collectives_main_hip from $DRV against include/hiccl.h"
+  fi
+fi

@@ -1,0 +1,50 @@
+"""Drop-in evidence: the reference's OWN driver, collectives/main.cpp, compiled
+unmodified against this build's include/hiccl.h (oracle/build_ref.sh; only in
+the build container, where /root/reference exists, and shipped prebuilt as
+oracle/_ref/collectives_main_{host,hip}).
+
+It composes the eight collectives from add_reduce / add_bcast / add_fence,
+sets its hard-coded {4,4,2} hierarchy with {MPI, IPC, IPC} (main.cpp:164-165),
+measures per command and per collective, and runs the reference's own
+known-answer test HiCCL::validate (bench.h:62-227) -- which must print
+PASSED on every run.  Host port on CPU; HIP port on the GPU (8 ranks share
+the box's MI355X).
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_HOST = os.path.join(ROOT, "oracle", "_ref", "collectives_main_host")
+REF_HIP = os.path.join(ROOT, "oracle", "_ref", "collectives_main_hip")
+MPIRUN = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
+NAMES = {1: "GATHER", 2: "SCATTER", 3: "BCAST", 4: "REDUCE", 5: "ALL-TO-ALL", 6: "ALL-GATHER",
+         7: "REDUCE-SCATTER", 8: "ALL-REDUCE"}
+
+
+def run(exe, np_, args, env_extra=None, timeout=240):
+    env = dict(os.environ, OMP_NUM_THREADS="1", HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_SIGNAL_TIMEOUT="10")
+    env.update(env_extra or {})
+    cmd = ["timeout", "-k", "10", str(timeout), MPIRUN, "-np", str(np_), exe] + [str(a) for a in args]
+    p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd="/tmp")
+    return p.returncode, p.stdout + p.stderr
+
+
+@pytest.mark.skipif(not os.path.exists(REF_HOST), reason="reference driver not built (needs /root/reference)")
+@pytest.mark.parametrize("np_,args", [(8, [1000, 1, 1, 4, 1, 2]), (8, [999, 2, 2, 3, 0, 1]),
+                                      (16, [257, 1, 1, 2, 0, 1])])
+@pytest.mark.parametrize("pattern", range(1, 9))
+def test_reference_driver_host(pattern, np_, args):
+    rc, out = run(REF_HOST, np_, [pattern] + args)
+    assert f"VERIFY {NAMES[pattern]} ROOT = 0: PASSED!" in out, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(REF_HIP), reason="reference driver not built (needs /root/reference)")
+@pytest.mark.parametrize("streamed", ["0", "1"], ids=["host", "stream"])
+@pytest.mark.parametrize("pattern", [4, 7, 8])
+def test_reference_driver_gpu(pattern, streamed):
+    rc, out = run(REF_HIP, 8, [pattern, 4099, 1, 1, 4, 1, 2], {"HICCL_STREAM_ORDERED": streamed})
+    assert f"VERIFY {NAMES[pattern]} ROOT = 0: PASSED!" in out, out[-3000:]
