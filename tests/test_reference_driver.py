@@ -44,7 +44,8 @@ def test_reference_driver_host(pattern, np_, args):
 @pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(REF_HIP), reason="reference driver not built (needs /root/reference)")
 @pytest.mark.parametrize("streamed", ["0", "1"], ids=["host", "stream"])
-@pytest.mark.parametrize("pattern", [4, 7, 8])
+@pytest.mark.parametrize("pattern", [7, 8])
 def test_reference_driver_gpu(pattern, streamed):
-    rc, out = run(REF_HIP, 8, [pattern, 4099, 1, 1, 4, 1, 2], {"HICCL_STREAM_ORDERED": streamed})
+    # 8 processes time-share one GPU here: keep the driver's own measure loops minimal
+    rc, out = run(REF_HIP, 8, [pattern, 4099, 1, 1, 4, 0, 1], {"HICCL_STREAM_ORDERED": streamed})
     assert f"VERIFY {NAMES[pattern]} ROOT = 0: PASSED!" in out, out[-3000:]
