@@ -127,6 +127,11 @@ class Comm {
   // faster; with one process per GPU this mode removes
   // every host round trip per step.
   void set_stream_ordered(bool on) { stream_req = on ? 1 : 0; }
+  // Fused gather + reduce (HIP port, IPC / IPC_get levels): a transfer whose
+  // receive buffer only feeds a reduction of the same step is not copied;
+  // the reduction kernel reads the sender's buffer over xGMI in place.
+  // Opt-in (HICCL_FUSED_GATHER=1 or this setter); results are identical.
+  void set_fused_gather(bool on) { fuse_req = on ? 1 : 0; }
   void set_endpoints(T *sb, size_t sc, T *rb, size_t rc) {
     sendbuf = sb;
     sendcount = sc;
@@ -208,8 +213,9 @@ class Comm {
     libs = libraries_used(coll_batch);
     steps = merge_steps(coll_batch, libs, 1);
     streamed = want_stream_mode();
+    fused = want_fused();
     CommBench::stream_ordered = streamed;
-    command_batch = instantiate(steps, libs);
+    command_batch = instantiate(steps, libs, fused);
     CommBench::stream_ordered = false;
 #ifndef HICCL_PORT_HOST
     if (streamed) {  // one flag pair per registered transfer, every rank the same layout
@@ -231,11 +237,12 @@ class Comm {
     MPI_Barrier(CommBench::comm_mpi);  // nobody runs before every rank's handles are exchanged
     report_memory();
     if (CommBench::myid == CommBench::printid)
-      std::printf("initialization time: %e seconds (%zu steps, %zu libraries, %s)\n", MPI_Wtime() - t0, steps.size(),
-                  libs.size(), streamed ? "stream-ordered" : "host-driven");
+      std::printf("initialization time: %e seconds (%zu steps, %zu libraries, %s%s)\n", MPI_Wtime() - t0, steps.size(),
+                  libs.size(), streamed ? "stream-ordered" : "host-driven", fused ? ", fused gather" : "");
   }
 
   bool stream_ordered() const { return streamed; }
+  bool fused_gather() const { return fused; }
 
   // ----------------------------------------------------------------- run --
   // comm.h:181-206
@@ -253,8 +260,9 @@ class Comm {
         it[i]->comm->wait();
         it[i]->compute->start();
       }
+      for (size_t i = 0; i < nl; i++) it[i]->compute->wait();
       for (size_t i = 0; i < nl; i++) {
-        it[i]->compute->wait();
+        it[i]->comm->finish();  // fused transfers: release the senders' buffers
         ++it[i];
       }
     }
@@ -328,6 +336,8 @@ class Comm {
 
   int stream_req = -1;  // -1: decide from the environment and the node layout
   bool streamed = false;
+  int fuse_req = -1;  // -1: HICCL_FUSED_GATHER
+  bool fused = false;
 #ifndef HICCL_PORT_HOST
   CommBench::FlagSpace flags;
 
@@ -344,7 +354,10 @@ class Comm {
     while (it[0] != command_batch[0].end()) {
       for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
       for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
-      for (size_t i = 0; i < nl; i++) ++it[i];
+      for (size_t i = 0; i < nl; i++) {
+        it[i]->comm->enqueue_tail(s);
+        ++it[i];
+      }
     }
     CommBench::hip_check(hipStreamSynchronize(s), "run: stream sync");
     if (*flags.err) CommBench::die("run", "stream-ordered signal timed out (a peer never signalled)");
@@ -368,6 +381,20 @@ class Comm {
     int ok = on && lsize == CommBench::numproc;
     MPI_Allreduce(MPI_IN_PLACE, &ok, 1, MPI_INT, MPI_LAND, CommBench::comm_mpi);
     return ok != 0;
+#endif
+  }
+
+  bool want_fused() {
+#ifdef HICCL_PORT_HOST
+    return false;
+#else
+    int on = fuse_req;
+    if (on < 0) {
+      const char *env = std::getenv("HICCL_FUSED_GATHER");
+      on = (env && std::string(env) == "1") ? 1 : 0;
+    }
+    MPI_Allreduce(MPI_IN_PLACE, &on, 1, MPI_INT, MPI_LAND, CommBench::comm_mpi);
+    return on != 0;
 #endif
   }
 

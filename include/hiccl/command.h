@@ -86,17 +86,24 @@ struct Command {
 
 // Build every step's transports and computes.  pipeline[i] is library i's
 // list of commands, one per step (the reference's command_batch).
+// `fuse`: transfers whose receive buffer only feeds a compute of the same
+// step (Coll::Xfer::feeds) are not copied; the compute reads the sender's
+// buffer in place through its IPC mapping (fused gather + reduce).
 template <typename T>
 std::vector<std::list<Command<T>>> instantiate(const std::vector<std::vector<Coll<T>>> &steps,
-                                               const std::vector<CommBench::library> &libs) {
+                                               const std::vector<CommBench::library> &libs, bool fuse = false) {
   std::vector<std::list<Command<T>>> pipeline(libs.size());
   for (auto &step : steps) {
     for (size_t i = 0; i < libs.size(); i++) {
       auto *comm = new CommBench::Comm<T>(libs[i]);
       auto *comp = new Compute<T>();
-      for (auto &x : step[i].xfers) comm->add(x.sendbuf, x.sendoffset, x.recvbuf, x.recvoffset, x.count, x.sendid, x.recvid);
+      for (auto &x : step[i].xfers)
+        comm->add(x.sendbuf, x.sendoffset, x.recvbuf, x.recvoffset, x.count, x.sendid, x.recvid, fuse && x.feeds);
       for (auto &c : step[i].comps) {
         std::vector<T *> in = c.inputs;
+        if (fuse && c.compid == CommBench::myid)
+          for (auto &p : in)
+            if (T *remote = comm->fused_source(p)) p = remote;
         comp->add(in, c.output, c.count, c.compid);
       }
       pipeline[i].emplace_back(comm, comp);

@@ -93,6 +93,7 @@ struct Coll {
     size_t recvoffset;
     size_t count;
     int sendid, recvid;
+    bool feeds;  // the receive buffer exists only to feed a compute of the same level
   };
   struct Comp {
     std::vector<T *> inputs;
@@ -105,8 +106,8 @@ struct Coll {
   std::vector<Comp> comps;
 
   explicit Coll(CommBench::library l) : lib(l) {}
-  void add(T *sb, size_t so, T *rb, size_t ro, size_t c, int sid, int rid) {
-    xfers.push_back({sb, so, rb, ro, c, sid, rid});
+  void add(T *sb, size_t so, T *rb, size_t ro, size_t c, int sid, int rid, bool feeds = false) {
+    xfers.push_back({sb, so, rb, ro, c, sid, rid, feeds});
   }
   void add(std::vector<T *> in, T *out, size_t c, int compid) { comps.push_back({std::move(in), out, c, compid}); }
   int numcomm() const { return (int)xfers.size(); }
@@ -195,7 +196,7 @@ class Planner {
               inputs.push_back(at(r.sendbuf, r.sendoffset));
             } else {
               T *rb = pooled(head, r.count, pool);
-              coll->add(r.sendbuf, r.sendoffset, rb, 0, r.count, s, head);
+              coll->add(r.sendbuf, r.sendoffset, rb, 0, r.count, s, head, true);
               inputs.push_back(rb);
             }
           }
@@ -273,7 +274,7 @@ class Planner {
       T *src = part;
       size_t src_off = part_off;
       if (me != fwd) src = nullptr;
-      coll->add(src, src_off, land, land_off, r.count, fwd, r.recvid);
+      coll->add(src, src_off, land, land_off, r.count, fwd, r.recvid, !local.empty());
     }
     if (!further.empty()) {
       reduce_ring(numlevel, gsz, lib, further, intra, out);

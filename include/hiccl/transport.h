@@ -358,8 +358,14 @@ class Comm {
   // Register one transfer: count elements from sendbuf+sendoffset on rank
   // sendid to recvbuf+recvoffset on rank recvid.  Pointers need only be
   // valid on their owning rank.
+  //
+  // `fused` (IPC / IPC_get only, decided identically on every rank): the
+  // bytes are not moved at all.  The receiver maps the sender's buffer and
+  // its compute reads it in place (fused_source); the sender's ready token
+  // precedes the compute and the receiver's done token follows it (finish /
+  // enqueue_tail), so the sender keeps the buffer intact until then.
   void add(T *sendbuf, size_t sendoffset, T *recvbuf, size_t recvoffset, size_t count, int sendid,
-           int recvid) {
+           int recvid, bool fused = false) {
     Xfer x;
     x.src = sendbuf ? sendbuf + sendoffset : nullptr;
     x.dst = recvbuf ? recvbuf + recvoffset : nullptr;
@@ -374,12 +380,12 @@ class Comm {
       return;
     }
 #ifndef HICCL_PORT_HOST
+    x.fused = fused && sendid != recvid && (lib == IPC || lib == IPC_get);
     if (sendid != recvid && (lib == IPC || lib == IPC_get)) {
       // the mover needs a mapping of the owner's buffer
-      const int owner = lib == IPC ? recvid : sendid;
-      const int mover = lib == IPC ? sendid : recvid;
+      const int owner = owner_of(x), mover = mover_of(x);
       if (myid == owner) {
-        IpcExport e = ipc_export(lib == IPC ? x.dst : x.src);
+        IpcExport e = ipc_export(owner == x.sendid ? x.src : x.dst);
         mpi_check(MPI_Send(&e, sizeof(e), MPI_BYTE, mover, x.tag, comm_mpi), "MPI_Send(ipc)");
       }
       if (myid == mover) {
@@ -394,6 +400,14 @@ class Comm {
     xfers.push_back(x);
   }
 
+  // On the receiver of a fused transfer whose destination is `dst`: the
+  // mapping of the sender's buffer, which the compute reads instead.
+  T *fused_source(const T *dst) const {
+    for (auto &x : xfers)
+      if (x.fused && x.recvid == myid && x.dst == dst) return reinterpret_cast<T *>(x.remote);
+    return nullptr;
+  }
+
 #ifndef HICCL_PORT_HOST
   // Stream-ordered mode: assign flag slots [2*base, 2*(base+size())) of fs.
   void bind(FlagSpace *fs, size_t base) {
@@ -402,31 +416,34 @@ class Comm {
     pre_wait.clear();
     post_sig.clear();
     post_wait.clear();
+    tail_sig.clear();
+    tail_wait.clear();
     for (size_t j = 0; j < xfers.size(); j++) {
       const Xfer &x = xfers[j];
       if (lib == dummy || x.count == 0 || x.sendid == x.recvid) continue;
-      const int owner = lib == IPC ? x.recvid : x.sendid;
-      const int mover = lib == IPC ? x.sendid : x.recvid;
+      const int owner = owner_of(x), mover = mover_of(x);
       const size_t ready = 2 * (base + j), done = ready + 1;
       if (myid == owner) {
         pre_sig.push_back(fs->peer[mover] + ready);
-        post_wait.push_back(fs->local + done);
+        (x.fused ? tail_wait : post_wait).push_back(fs->local + done);
       }
       if (myid == mover) {
         pre_wait.push_back(fs->local + ready);
-        post_sig.push_back(fs->peer[owner] + done);
+        (x.fused ? tail_sig : post_sig).push_back(fs->peer[owner] + done);
       }
     }
   }
 
   // Enqueue one execution on `s` without waiting: owners signal ready,
-  // movers wait for ready, copy, signal done, owners wait for done.
+  // movers wait for ready, copy, signal done, owners wait for done.  The
+  // done tokens of fused transfers follow the step's compute: enqueue_tail.
   void enqueue(hipStream_t s) {
     ++epoch;
     signal_wait(pre_sig, pre_wait, epoch, flags->err, s);
     launch_copies(s);
     signal_wait(post_sig, post_wait, epoch, flags->err, s);
   }
+  void enqueue_tail(hipStream_t s) { signal_wait(tail_sig, tail_wait, epoch, flags->err, s); }
 
   bool stream_mode() const { return streamed; }
 #endif
@@ -437,12 +454,15 @@ class Comm {
     if (streamed) {
       if (!flags) die("transport", "stream-ordered Comm used before bind()");
       enqueue(stream);
+      enqueue_tail(stream);  // standalone use (measure): no compute in between
       return;
     }
     build_plans();
 #endif
     reqs.clear();
     movers.clear();
+    readers.clear();
+    tail_reqs.clear();
     issued = false;
 #ifndef HICCL_PORT_HOST
     if (selfplan) {
@@ -477,13 +497,18 @@ class Comm {
         continue;
       }
 #ifndef HICCL_PORT_HOST
-      const bool mover = lib == IPC ? me_send : me_recv;
+      const bool mover = myid == mover_of(x);
       if (mover) {
-        movers.push_back({&x, (int)reqs.size()});
+        (x.fused ? readers : movers).push_back({&x, (int)reqs.size()});
         post(MPI_Irecv(nullptr, 0, MPI_BYTE, peer, x.tag, comm_mpi, next()));  // ready
       } else {
         post(MPI_Isend(nullptr, 0, MPI_BYTE, peer, x.tag, comm_mpi, next()));  // ready
-        post(MPI_Irecv(nullptr, 0, MPI_BYTE, peer, x.tag + 30000, comm_mpi, next()));  // done
+        if (x.fused) {
+          tail_reqs.emplace_back();  // done: after the reader's compute, in finish()
+          post(MPI_Irecv(nullptr, 0, MPI_BYTE, peer, x.tag + 30000, comm_mpi, &tail_reqs.back()));
+        } else {
+          post(MPI_Irecv(nullptr, 0, MPI_BYTE, peer, x.tag + 30000, comm_mpi, next()));  // done
+        }
       }
 #endif
     }
@@ -498,6 +523,7 @@ class Comm {
       return;
     }
     for (auto &m : movers) mpi_check(MPI_Wait(&reqs[m.req], MPI_STATUS_IGNORE), "MPI_Wait(ready)");
+    for (auto &m : readers) mpi_check(MPI_Wait(&reqs[m.req], MPI_STATUS_IGNORE), "MPI_Wait(ready)");
     if (!movers.empty() && moveplan) launch_plan(moveplan, stream, "IPC moves");  // every move, one kernel
     if (issued || !movers.empty()) hip_check(hipStreamSynchronize(stream), "transport stream sync");
     for (auto &m : movers) {
@@ -518,6 +544,23 @@ class Comm {
 #endif
   }
 
+  // After the step's compute (host-driven mode): readers of fused transfers
+  // release the senders' buffers; senders wait for that release.
+  void finish() {
+#ifndef HICCL_PORT_HOST
+    if (streamed) return;
+    for (auto &m : readers) {
+      const int peer = m.x->sendid;
+      tail_reqs.emplace_back();
+      post(MPI_Isend(nullptr, 0, MPI_BYTE, peer, m.x->tag + 30000, comm_mpi, &tail_reqs.back()));
+    }
+    if (!tail_reqs.empty())
+      mpi_check(MPI_Waitall((int)tail_reqs.size(), tail_reqs.data(), MPI_STATUSES_IGNORE), "MPI_Waitall(done)");
+    tail_reqs.clear();
+    readers.clear();
+#endif
+  }
+
   // Per-step transport micro-benchmark (CommBench::Comm::measure call site:
   // command.h:21).  Prints min/median/max like the reference's tables.
   void measure(int warmup, int numiter, size_t count) {
@@ -527,6 +570,7 @@ class Comm {
       double t0 = MPI_Wtime();
       start();
       wait();
+      finish();
       double dt = MPI_Wtime() - t0;
       MPI_Allreduce(MPI_IN_PLACE, &dt, 1, MPI_DOUBLE, MPI_MAX, comm_mpi);
       if (it >= 0) t.push_back(dt);
@@ -549,21 +593,27 @@ class Comm {
     T *staging = nullptr;    // pinned host staging (MPI with device memory)
     size_t count = 0;
     int sendid = 0, recvid = 0, tag = 0;
+    bool fused = false;  // no bytes move: the receiver's compute reads `remote`
   };
+  // IPC: the sender moves into the receiver's buffer; IPC_get and fused
+  // transfers: the receiver maps the sender's buffer.
+  int owner_of(const Xfer &x) const { return lib == IPC && !x.fused ? x.recvid : x.sendid; }
+  int mover_of(const Xfer &x) const { return lib == IPC && !x.fused ? x.sendid : x.recvid; }
   struct Mover {
     Xfer *x;
     int req;
   };
   std::vector<Xfer> xfers;
   std::vector<MPI_Request> reqs;
-  std::vector<Mover> movers;
+  std::vector<Mover> movers, readers;
+  std::vector<MPI_Request> tail_reqs;
   bool issued = false;  // async device work enqueued by start()
 #ifndef HICCL_PORT_HOST
   hipStream_t stream = nullptr;
   bool streamed = false;
   FlagSpace *flags = nullptr;
   uint32_t epoch = 0;
-  std::vector<uint32_t *> pre_sig, pre_wait, post_sig, post_wait;
+  std::vector<uint32_t *> pre_sig, pre_wait, post_sig, post_wait, tail_sig, tail_wait;
   // batched exact copies (HICCL_BYTES plans): the bytes this rank moves to or
   // from peers, and its self transfers -- one kernel each per execution
   hiccl_reduce_plan_t *moveplan = nullptr, *selfplan = nullptr;
@@ -576,8 +626,7 @@ class Comm {
     for (const Xfer &x : xfers) {
       if (!x.count) continue;
       const bool self = x.sendid == x.recvid && x.sendid == myid;
-      const bool move = x.sendid != x.recvid && (lib == IPC || lib == IPC_get) &&
-                        myid == (lib == IPC ? x.sendid : x.recvid);
+      const bool move = x.sendid != x.recvid && !x.fused && (lib == IPC || lib == IPC_get) && myid == mover_of(x);
       if (!self && !move) continue;
       hiccl_reduce_plan_t *&p = self ? selfplan : moveplan;
       if (!p && hiccl_reduce_plan_create(&p, HICCL_BYTES, mydevice)) die("transport", hiccl_last_error());

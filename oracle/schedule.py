@@ -419,6 +419,11 @@ def implement(coll_batch, pipeoffset=1):
     return steps
 
 
+class Remote(tuple):
+    """A compute input read in place on another rank (fused gather +
+    reduce: the transfer that fed this input was dropped).  Remote((rank, loc))."""
+
+
 def simulate(steps, numproc, user, dtype=np.float32):
     """Execute the plan.  user: {(rank, name): array}.  Temporaries are
     created on first write.  Comms of a step run before its computes (the
@@ -449,7 +454,7 @@ def simulate(steps, numproc, user, dtype=np.float32):
                 for (r, ins, out, cnt) in step[lib].computes:
                     acc = np.zeros(cnt, dtype)
                     for loc in ins:
-                        a, o = view(r, loc, cnt)
+                        a, o = view(*loc, cnt) if isinstance(loc, Remote) else view(r, loc, cnt)
                         acc = (acc + a[o:o + cnt]).astype(dtype)
                     oa, oo = view(r, out, cnt)
                     oa[oo:oo + cnt] = acc

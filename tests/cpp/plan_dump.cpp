@@ -93,7 +93,7 @@ int main(int argc, char **argv) {
           print_ptr(r == x.sendid ? HiCCL::at(x.sendbuf, x.sendoffset) : nullptr);
           std::printf(",\"dst\":");
           print_ptr(r == x.recvid ? HiCCL::at(x.recvbuf, x.recvoffset) : nullptr);
-          std::printf("}\n");
+          std::printf(",\"feeds\":%s}\n", x.feeds ? "true" : "false");
         }
         for (const auto &k : c.comps) {
           if (k.compid != r) continue;  // Compute::add records on the owner only

@@ -28,10 +28,10 @@ HIP = os.path.join(ROOT, "build", "collectives_hip")
 HIP_F32 = os.path.join(ROOT, "build", "collectives_hip_f32")
 
 
-def mpirun(np_, exe, args, timeout=180, streamed=True):
+def mpirun(np_, exe, args, timeout=180, streamed=True, fused=False):
     assert np_ <= 8
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED="1" if streamed else "0",
-               HICCL_SIGNAL_TIMEOUT="10")
+               HICCL_FUSED_GATHER="1" if fused else "0", HICCL_SIGNAL_TIMEOUT="10")
     cmd = ["timeout", "-k", "10", str(timeout), MPIRUN, "-np", str(np_), exe] + [str(a) for a in args]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd="/tmp")
     return p.returncode, p.stdout + p.stderr
@@ -48,16 +48,31 @@ def test_known_answer(np_, hier, libs, pattern, streamed):
     assert ("stream-ordered" if streamed else "host-driven") in out
 
 
+@pytest.mark.parametrize("streamed", [True, False], ids=["stream", "host"])
+@pytest.mark.parametrize("np_,hier,libs", [(2, "2", "ipc"), (4, "4", "ipc_get"), (8, "1,4,2", "mpi,ipc,ipc"),
+                                           (8, "2,4", "ipc,ipc_get")])
+@pytest.mark.parametrize("pattern", [4, 7, 8])
+def test_known_answer_fused_gather(np_, hier, libs, pattern, streamed):
+    """HICCL_FUSED_GATHER=1: reductions read peers' buffers in place."""
+    rc, out = mpirun(np_, HIP, [pattern, 4099, 1, 1, 3, 0, 0, hier, libs], streamed=streamed, fused=True)
+    assert rc == 0, out[-3000:]
+    assert "PASSED!" in out
+    assert "fused gather" in out
+
+
 @pytest.mark.parametrize("np_,count,stripe,ring,depth,hier,libs", [
     (2, 65536, 1, 1, 4, "2", "ipc"),
     (4, 10007, 1, 1, 3, "2,2", "mpi,ipc"),
     (8, 4099, 1, 1, 4, "1,4,2", "mpi,ipc,ipc"),
     (8, 4099, 1, 2, 2, "2,4", "ipc,ipc_get"),
 ])
-@pytest.mark.parametrize("streamed", [True, False], ids=["stream", "host"])
-def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ring, depth, hier, libs, streamed):
+@pytest.mark.parametrize("streamed,fused", [(True, False), (False, False), (True, True), (False, True)],
+                         ids=["stream", "host", "stream-fused", "host-fused"])
+def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ring, depth, hier, libs, streamed,
+                                        fused):
     prefix = str(tmp_path / "ar")
-    rc, out = mpirun(np_, HIP_F32, [8, count, stripe, ring, depth, 0, 0, hier, libs, prefix], streamed=streamed)
+    rc, out = mpirun(np_, HIP_F32, [8, count, stripe, ring, depth, 0, 0, hier, libs, prefix], streamed=streamed,
+                     fused=fused)
     assert rc == 0, out[-3000:]
     n = count * np_
     x = {r: oracle.fill(r + 1, n, 1234)[r] for r in range(np_)}

@@ -44,7 +44,10 @@ def run_dump(np_, pattern, count, stripe, ring, depth, hier, libs):
     return [json.loads(line) for line in out.splitlines()]
 
 
-def simulate_dump(recs, np_, count, x):
+def simulate_dump(recs, np_, count, x, fuse=False):
+    """fuse=True executes the plan as HICCL_FUSED_GATHER does: transfers
+    marked `feeds` are dropped and the compute reads the sender's buffer in
+    place (oracle/schedule.py Remote)."""
     allocs = {}
     for r in recs:
         if r["kind"] == "alloc":
@@ -71,18 +74,25 @@ def simulate_dump(recs, np_, count, x):
     for r in recs:
         if r["kind"] == "xfer":
             key = (r["step"], r["lib"], r["idx"])
-            e = xf.setdefault(key, {"sendid": r["sendid"], "recvid": r["recvid"], "count": r["count"]})
-            assert (e["sendid"], e["recvid"], e["count"]) == (r["sendid"], r["recvid"], r["count"]), key
+            e = xf.setdefault(key, {"sendid": r["sendid"], "recvid": r["recvid"], "count": r["count"],
+                                    "feeds": r["feeds"]})
+            assert (e["sendid"], e["recvid"], e["count"], e["feeds"]) == \
+                (r["sendid"], r["recvid"], r["count"], r["feeds"]), key  # every rank plans the same
             if r["rank"] == r["sendid"]:
                 e["src"] = loc(r["rank"], r["src"])
             if r["rank"] == r["recvid"]:
                 e["dst"] = loc(r["rank"], r["dst"])
+    fused = {}  # (step, lib, recvid, dst) -> Remote((sendid, src))
     for (s, lib, idx) in sorted(xf):
         e = xf[(s, lib, idx)]
+        if fuse and e["feeds"] and e["sendid"] != e["recvid"]:
+            fused[(s, lib, e["recvid"], e["dst"])] = S.Remote((e["sendid"], e["src"]))
+            continue
         steps[s][lib].add_comm(e["sendid"], e["src"], e["recvid"], e["dst"], e["count"])
     for r in recs:
         if r["kind"] == "comp":
             ins = [loc(r["rank"], a) for a in r["in"]]
+            ins = [fused.get((r["step"], r["lib"], r["rank"], i), i) for i in ins]
             steps[r["step"]][r["lib"]].add_compute(r["rank"], ins, loc(r["rank"], r["out"]), r["count"])
     user = {}
     for rank in range(np_):
@@ -188,3 +198,69 @@ def test_ring_single_rank_nodes_reference_defect():
     assert np.allclose(cmem[(0, ("recv",))], exact, rtol=1e-5, atol=1e-4)
     assert not np.allclose(ref[(0, ("recv",))], exact, rtol=1e-5, atol=1e-4)
     assert any(ref[(r, ("send",))].tobytes() != x[r].tobytes() for r in range(np_))
+
+
+def fused_hazards(recs):
+    """Static conditions for dropping a `feeds` transfer (comm.h fused
+    gather): (1) its receive buffer is an input of exactly one compute of the
+    same step and library on the receiver; (2) nothing writes the sender's
+    source during that step; (3) no later step reads the receive buffer
+    before writing it."""
+    problems = []
+    feeds = [r for r in recs if r["kind"] == "xfer" and r["feeds"] and r["rank"] == r["recvid"]]
+    srcs = {(r["step"], r["lib"], r["idx"]): r for r in recs if r["kind"] == "xfer" and r["rank"] == r["sendid"]}
+    comps = [r for r in recs if r["kind"] == "comp"]
+    writes = {}  # (step, rank) -> [(addr, nbytes)]
+    for r in recs:
+        if r["kind"] == "xfer" and r["rank"] == r["recvid"]:
+            writes.setdefault((r["step"], r["rank"]), []).append((r["dst"], 4 * r["count"]))
+        if r["kind"] == "comp":
+            writes.setdefault((r["step"], r["rank"]), []).append((r["out"], 4 * r["count"]))
+    ov = lambda a, n, b, m: a < b + m and b < a + n  # noqa: E731
+    for f in feeds:
+        if f["sendid"] == f["recvid"]:
+            continue
+        nb = 4 * f["count"]
+        uses = sum(i == f["dst"] for c in comps if (c["step"], c["lib"], c["rank"]) == (f["step"], f["lib"], f["recvid"])
+                   for i in c["in"])
+        if uses != 1:
+            problems.append(("uses", f, uses))
+        src = srcs[(f["step"], f["lib"], f["idx"])]["src"]
+        for (a, n) in writes.get((f["step"], f["sendid"]), []):
+            if ov(a, n, src, nb):
+                problems.append(("src written", f))
+        for t in range(f["step"] + 1, max(r.get("step", 0) for r in recs) + 1):
+            rd = [r for r in recs if r.get("step") == t and r["rank"] == f["recvid"]]
+            if any(r["kind"] == "xfer" and r["rank"] == r["sendid"] and ov(r["src"], 4 * r["count"], f["dst"], nb)
+                   for r in rd):
+                problems.append(("read later", f, t))
+                break
+            if any(r["kind"] == "xfer" and r["rank"] == r["recvid"] and ov(r["dst"], 4 * r["count"], f["dst"], nb)
+                   for r in rd):
+                break
+            if any(r["kind"] == "comp" and any(ov(i, 4 * r["count"], f["dst"], nb) for i in r["in"]) for r in rd):
+                problems.append(("read later", f, t))
+                break
+            if any(r["kind"] == "comp" and ov(r["out"], 4 * r["count"], f["dst"], nb) for r in rd):
+                break
+    return problems
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: f"P{c[0]}-{c[1]}-s{c[3]}r{c[4]}d{c[5]}-{'x'.join(map(str, c[6]))}")
+def test_fused_gather_plan(cfg):
+    """SURVEY.md 8 row f: the fused gather + reduce executes the same plan
+    minus the `feeds` copies, reading senders' buffers in place; the results
+    must equal the unfused oracle bit for bit and the plan must be free of the
+    hazards dropping those copies could expose."""
+    np_, pattern, count, stripe, ring, depth, hier, libs = cfg
+    x = inputs(np_, count * np_)
+    recs = run_dump(np_, pattern, count, stripe, ring, depth, hier, libs)
+    assert fused_hazards(recs) == []
+    _, fmem = simulate_dump(recs, np_, count, x, fuse=True)
+    _, omem = oracle_run(np_, pattern, count, stripe, ring, depth, hier, libs, x)
+    nfeeds = sum(r["kind"] == "xfer" and r["feeds"] and r["rank"] == r["recvid"] for r in recs)
+    if pattern in ("reduce", "allreduce", "reducescatter"):
+        assert nfeeds > 0
+    for rank in range(np_):
+        a, b = fmem[(rank, ("recv",))], omem[(rank, ("recv",))]
+        assert a.tobytes() == b.tobytes(), f"rank {rank}: {int((a != b).sum())} elements differ"
