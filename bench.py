@@ -294,6 +294,7 @@ def main():
     ap.add_argument("--nway", action="store_true")
     ap.add_argument("--chunks", action="store_true")
     ap.add_argument("--roundtrip", action="store_true")
+    ap.add_argument("--c2variants", action="store_true")
     args = ap.parse_args()
 
     dist = Dist(args.gpus)
@@ -303,6 +304,8 @@ def main():
         return nway(args)
     if args.chunks:
         return chunks(args)
+    if args.c2variants:
+        return c2variants(args)
     if args.roundtrip:
         return roundtrip(args)
 
@@ -450,6 +453,35 @@ def nway(args):
                           "read_GBps": round(n * count * 4 / t / 1e9, 1),
                           "frac_of_copy": round(b / t / 1e9 / copy_gbps, 4)}), flush=True)
         del ins, out
+        torch.cuda.empty_cache()
+    return 0
+
+
+def c2variants(args):
+    """Config 2 variants: the README's count 1e9/sizeof(T)
+    = 2.5e8 (tail handling), and the 2^28 bucket with every input shifted by
+    1-3 elements and the output by 0 or 1 (the mutual misalignment partition()
+    produces)."""
+    n = 8
+    cases = [("readme_count", 250_000_000, [0] * n, 0),
+             ("inputs_shifted", 1 << 28, [1 + k % 3 for k in range(n)], 0),
+             ("inputs_and_output_shifted", 1 << 28, [1 + k % 3 for k in range(n)], 1)]
+    for name, count, in_off, out_off in cases:
+        bases = [torch.empty(count + 4, dtype=torch.float32, device="cuda") for _ in range(n)]
+        ins = [b[o:o + count] for b, o in zip(bases, in_off)]
+        for k, t in enumerate(ins):
+            hiccl_amd.fill_uniform(t, SEED, k)
+        obase = torch.empty(count + 4, dtype=torch.float32, device="cuda")
+        out = obase[out_off:out_off + count]
+        torch.cuda.synchronize()
+        _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins), args.steps, args.warmup)
+        t = float(np.median(ms)) * 1e-3
+        b = (n + 1) * count * 4
+        print(json.dumps({"config": "C2", "variant": name, "count": count, "input_offsets": in_off,
+                          "output_offset": out_off, "parity_sample_ok": sample_check(out, n, count),
+                          "kernel_ms": round(t * 1e3, 4), "GBps": round(b / t / 1e9, 1),
+                          "frac_hbm": round(b / t / 1e9 / HBM_PEAK_GBPS, 4)}), flush=True)
+        del bases, ins, obase, out
         torch.cuda.empty_cache()
     return 0
 

@@ -235,10 +235,12 @@ def test_plan_launch_from_other_thread(oracle):
     assert bits_equal(out.cpu().numpy(), oracle.reduce(list(x)))
 
 
-def test_full_size_sampled(oracle):
-    """Config 2 shape (8 x 2^28 f32) checked at 4096 random indices plus the
-    ends: a size-independent property check against the oracle's generator."""
-    n, count, seed = 8, 1 << 28, 1234
+@pytest.mark.parametrize("count", [1 << 28, 250_000_000], ids=["2^28", "readme_2.5e8"])
+def test_full_size_sampled(oracle, count):
+    """Config 2 shape (8 x 2^28 f32, and the README's 1e9/sizeof(float)
+    count for tail handling) checked at 4096 random indices plus the ends: a
+    size-independent property check against the oracle's generator."""
+    n, seed = 8, 1234
     free, _ = torch.cuda.mem_get_info()
     if free < (n + 2) * count * 4:
         pytest.skip("not enough device memory")
