@@ -125,6 +125,10 @@ class Compute {
   // price `count` elements (the caller's choice, as the reference does).
   void measure(int warmup, int numiter, size_t cnt) {
     report();
+    unsigned long busiest = 0;  // algorithmic bytes (n reads + 1 write) of the busiest rank
+    for (int c = 0; c < numcomp; c++) busiest += (unsigned long)(count[c] * (inputbuf[c].size() + 1) * sizeof(T));
+    MPI_Allreduce(MPI_IN_PLACE, &busiest, 1, MPI_UNSIGNED_LONG, MPI_MAX, CommBench::comm_mpi);
+    roofline_bytes = (double)busiest;
     std::vector<double> times;
     if (CommBench::myid == CommBench::printid) {
       std::printf("Measure Reduction Kernel\n%d warmup iterations (in order)\n", warmup);
@@ -148,15 +152,20 @@ class Compute {
       }
     }
     print_times(times, (double)cnt * sizeof(T));
+    roofline_bytes = 0;
   }
 
-  // compute.h:251-257: price reads + writes, sum over ranks.
+  // compute.h:251-257: price reads + writes, sum over ranks.  Also prints
+  // the per-GPU HBM roofline fraction: the busiest rank's algorithmic bytes
+  // over the median time against the 8 TB/s MI355X peak.
   void measure(int warmup, int numiter) {
     size_t tot = 0;
     for (int c = 0; c < numcomp; c++) tot += count[c] * (inputbuf[c].size() + 1);
     MPI_Allreduce(MPI_IN_PLACE, &tot, 1, MPI_UNSIGNED_LONG, MPI_SUM, CommBench::comm_mpi);
     measure(warmup, numiter, tot);
   }
+
+  static constexpr double hbm_peak = 8.0e12;  // MI355X HBM3E, bytes/s
 
   static void print_times(std::vector<double> &times, double data) {
     if (times.empty() || CommBench::myid != CommBench::printid) return;
@@ -175,8 +184,15 @@ class Compute {
     const char *name[4] = {"min", "med", "max", "avg"};
     for (int i = 0; i < 4; i++)
       std::printf("%sTime: %.4e us, %.4e ms/GB, %.4e GB/s\n", name[i], v[i] * 1e6, v[i] / data * 1e12, data / v[i] / 1e9);
+#ifndef HICCL_PORT_HOST
+    if (roofline_bytes > 0)
+      std::printf("HBM roofline (busiest rank, median): %.1f GB/s = %.1f %% of %.0f GB/s\n",
+                  roofline_bytes / v[1] / 1e9, 100.0 * roofline_bytes / v[1] / hbm_peak, hbm_peak / 1e9);
+#endif
     std::printf("\n");
   }
+
+  static inline double roofline_bytes = 0;  // set by measure(warmup, numiter)
 
  private:
 #ifndef HICCL_PORT_HOST
