@@ -62,7 +62,8 @@ class Dist:
                 log(f"bench: WORLD_SIZE={self.world} but --gpus {gpus}")
         ndev = torch.cuda.device_count()
         self.device = self.local % max(ndev, 1)
-        torch.cuda.set_device(self.device)
+        if ndev:  # (no device: only the control plane, as in tests/test_bench_dist.py)
+            torch.cuda.set_device(self.device)
         self.pg = None
         self.backend = None
         if self.world > 1:
@@ -97,6 +98,12 @@ class Dist:
     def close(self):
         if self.pg:
             self.pg.destroy_process_group()
+
+
+def whole_job_gbps(world, bytes_per_step, steps, wall_max_s):
+    """Every rank reduces its own bucket (replicas): the job moves world x
+    bytes_per_step per step, and the job's time is the slowest rank's."""
+    return world * bytes_per_step * steps / wall_max_s / 1e9
 
 
 # ----------------------------------------------------------- workloads -----
@@ -319,7 +326,7 @@ def main():
     wall, kms = time_launches(step, args.steps, args.warmup, dist)
     wall_max = dist.max(wall)
     bytes_step = (n + 1) * count * 4
-    value = dist.world * bytes_step * args.steps / wall_max / 1e9
+    value = whole_job_gbps(dist.world, bytes_step, args.steps, wall_max)
     kern_s = float(np.mean(kms)) * 1e-3
     achieved = bytes_step / kern_s / 1e9
 
