@@ -297,6 +297,7 @@ def main():
     ap.add_argument("--nt", type=int, default=-1)
     ap.add_argument("--grid", type=int, default=0)
     ap.add_argument("--store", type=int, default=-1)
+    ap.add_argument("--engine", type=int, default=0, help="0 auto, 1 tile, 2 phase")
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--nway", action="store_true")
     ap.add_argument("--chunks", action="store_true")
@@ -318,9 +319,10 @@ def main():
 
     n, count = args.n, 1 << args.log2count
     cfg = None
-    if args.block or args.unroll or args.bpc or args.grid or args.nt >= 0 or args.store >= 0:
+    if args.block or args.unroll or args.bpc or args.grid or args.nt >= 0 or args.store >= 0 or args.engine:
         cfg = dict(block=args.block, unroll=args.unroll, blocks_per_cu=args.bpc, grid=args.grid,
-                   nontemporal=args.nt + 1 if args.nt >= 0 else 0, store_policy=args.store + 1 if args.store >= 0 else 0)
+                   nontemporal=args.nt + 1 if args.nt >= 0 else 0, store_policy=args.store + 1 if args.store >= 0 else 0,
+                   engine=args.engine)
     ins, out = make_bucket(n, count)
     step = lambda: hiccl_amd.reduce(out, ins, config=cfg)  # noqa: E731
     wall, kms = time_launches(step, args.steps, args.warmup, dist)
@@ -398,14 +400,12 @@ def sweep(args):
     no-arithmetic 8R+1W probe (tools/libhbm_probe.so) as the ceiling row."""
     n, count = args.n, 1 << args.log2count
     ins, out = make_bucket(n, count)
-    variants = []
-    for block in (256, 512):
-        for unroll in (2, 4):
-            for nt in (1, 2):
-                for store in (1, 2, 3):
-                    for grid in (192, 256, 512, 1024):
-                        variants.append(dict(block=block, unroll=unroll, nontemporal=nt, store_policy=store,
-                                             grid=grid))
+    variants = [dict(engine=1), dict(engine=1, grid=192), dict(engine=1, block=512, unroll=4, grid=512)]
+    for shape in ((512, 16), (1024, 4), (512, 8), (1024, 8), (256, 16)):
+        for grid in (0, 512):
+            variants.append(dict(engine=2, block=shape[0], unroll=shape[1], grid=grid))
+    for nt, store in ((1, 1), (1, 2), (2, 1), (2, 3)):
+        variants.append(dict(engine=2, nontemporal=nt, store_policy=store))
     probe = None
     pso = os.path.join(ROOT, "tools", "libhbm_probe.so")
     if os.path.exists(pso):
@@ -451,16 +451,19 @@ def nway(args):
     count = 1 << 26
     copy_gbps = copy_ceiling()
     for n in (2, 3, 4, 8, 16, 32, 64):
-        ins, out = make_bucket(n, count)
-        _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins), args.steps, args.warmup)
+      ins, out = make_bucket(n, count)
+      for eng in (0, 1):  # auto (= phase at this size), tile
+        cfg = dict(engine=eng) if eng else None
+        _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins, config=cfg), args.steps, args.warmup)
         t = float(np.median(ms)) * 1e-3
         b = (n + 1) * count * 4
-        print(json.dumps({"config": "C3", "n": n, "count": count, "kernel_ms": round(t * 1e3, 4),
+        print(json.dumps({"config": "C3", "engine": ["auto", "tile"][eng], "n": n, "count": count,
+                          "kernel_ms": round(t * 1e3, 4),
                           "GBps": round(b / t / 1e9, 1), "frac_hbm": round(b / t / 1e9 / HBM_PEAK_GBPS, 4),
                           "read_GBps": round(n * count * 4 / t / 1e9, 1),
                           "frac_of_copy": round(b / t / 1e9 / copy_gbps, 4)}), flush=True)
-        del ins, out
-        torch.cuda.empty_cache()
+      del ins, out
+      torch.cuda.empty_cache()
     return 0
 
 

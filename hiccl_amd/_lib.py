@@ -28,6 +28,10 @@ HICCL_BYTES = 5
 HICCL_ACC_NATIVE = 0
 HICCL_ACC_WIDE = 1
 
+HICCL_ENGINE_AUTO = 0
+HICCL_ENGINE_TILE = 1
+HICCL_ENGINE_PHASE = 2
+
 DTYPE_OF_TORCH = {
     torch.float32: HICCL_FLOAT32,
     torch.float64: HICCL_FLOAT64,
@@ -49,7 +53,8 @@ class HicclError(RuntimeError):
 class ReduceConfig(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("unroll", ctypes.c_int),
                 ("blocks_per_cu", ctypes.c_int), ("nontemporal", ctypes.c_int),
-                ("acc", ctypes.c_int), ("grid", ctypes.c_int), ("store_policy", ctypes.c_int)]
+                ("acc", ctypes.c_int), ("grid", ctypes.c_int), ("store_policy", ctypes.c_int),
+                ("engine", ctypes.c_int)]
 
 
 _lib = None
@@ -66,6 +71,8 @@ _SIGS = {
                                        ctypes.POINTER(ReduceConfig)]),
     "hiccl_reduce_plan_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int]),
     "hiccl_reduce_plan_set_acc": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "hiccl_reduce_plan_set_engine": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "hiccl_reduce_plan_engine": (ctypes.c_int, [_vp]),
     "hiccl_reduce_plan_add": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_size_t]),
     "hiccl_reduce_plan_launch": (ctypes.c_int, [_vp, _vp]),
     "hiccl_reduce_plan_launch_each": (ctypes.c_int, [_vp, _vp]),

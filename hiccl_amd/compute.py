@@ -104,7 +104,8 @@ class Compute:
     measure(warmup, numiter[, count])  compute.h:191-257.
     """
 
-    def __init__(self, dtype=torch.float32, device=None, myid=0, acc=L.HICCL_ACC_NATIVE):
+    def __init__(self, dtype=torch.float32, device=None, myid=0, acc=L.HICCL_ACC_NATIVE,
+                 engine=L.HICCL_ENGINE_AUTO):
         self.dtype = dtype
         self.code = L.DTYPE_OF_TORCH[dtype]
         if device is None:
@@ -121,6 +122,12 @@ class Compute:
         self._plan = h
         if acc != L.HICCL_ACC_NATIVE:
             L.check(L.lib().hiccl_reduce_plan_set_acc(self._plan, acc), "plan_set_acc")
+        if engine != L.HICCL_ENGINE_AUTO:
+            L.check(L.lib().hiccl_reduce_plan_set_engine(self._plan, engine), "plan_set_engine")
+
+    def engine(self):
+        """Engine the last upload resolved to (HICCL_ENGINE_TILE / _PHASE)."""
+        return L.lib().hiccl_reduce_plan_engine(self._plan)
 
     @staticmethod
     def _ptr(buf, esz):

@@ -32,6 +32,7 @@
 
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/hiccl_reduce.h"
@@ -332,6 +333,73 @@ __device__ __forceinline__ void tile_body(char *outb, Inputs in, uint32_t n, uin
   for (int u = 0; u < U; u++) store_pkt<POL>(w, voff[u], Op::pack(acc[u]));
 }
 
+// Input-phased chunk (the default engine for large buckets).  A chunk =
+// BLOCK*P packets; lane t owns packets p*BLOCK + t.  The workgroup sweeps
+// input 0 of the chunk, then input 1, ...: input j+1's P loads are in flight
+// while input j is added, so chip-wide only ~2 input streams are open at a
+// time and each is read as long contiguous runs (BLOCK*P*16 B per workgroup;
+// 128 KiB at the default 512 x 16).  The per-element add order is unchanged
+// (k = 0, 1, ..., n-1 from a zero accumulator).  Measured: the nine-stream
+// tile order runs at 5.5-5.8 TB/s and depends on the physical placement of
+// the buckets; the phased order at 6.0-6.4 TB/s.
+// n is runtime: inputs are taken in pairs; the load that would read past
+// input n-1 gets a zero-range descriptor (no memory traffic, reads 0, never
+// added).
+template <class Op, int P, int POL, class Inputs>
+__device__ __forceinline__ void chunk_body(char *outb, Inputs in, uint32_t n, uint64_t off,
+                                           uint32_t nbytes, const uint32_t (&voff)[P]) {
+  typename Op::acc_t acc[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) acc[p] = Op::zero();
+  if (n > 0) {
+    u32x4 x[P], y[P];
+    {
+      rsrc_t r = make_rsrc(in(0) + off, nbytes);
+#pragma unroll
+      for (int p = 0; p < P; p++) x[p] = load_pkt<POL>(r, voff[p]);
+    }
+    uint32_t j = 0;
+    for (; j + 2 <= n; j += 2) {  // x: input j in flight
+      rsrc_t ry = make_rsrc(in(j + 1) + off, nbytes);
+#pragma unroll
+      for (int p = 0; p < P; p++) y[p] = load_pkt<POL>(ry, voff[p]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] = Op::add(acc[p], x[p]);
+      __builtin_amdgcn_sched_barrier(0);
+      const bool more = j + 2 < n;
+      rsrc_t rx = make_rsrc(in(more ? j + 2 : j + 1) + off, more ? nbytes : 0u);
+#pragma unroll
+      for (int p = 0; p < P; p++) x[p] = load_pkt<POL>(rx, voff[p]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] = Op::add(acc[p], y[p]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (n & 1) {
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] = Op::add(acc[p], x[p]);
+    }
+  }
+  rsrc_t w = make_rsrc(outb + off, nbytes);
+#pragma unroll
+  for (int p = 0; p < P; p++) store_pkt<POL>(w, voff[p], Op::pack(acc[p]));
+}
+
+// Engines: kTile = all n inputs of a BLOCK*U tile loaded together (small
+// computes, many tiles); kPhase = chunk_body (large buckets).
+constexpr int kTile = 0;
+constexpr int kPhase = 1;
+
+template <class Op, int U, int POL, int ENG, class Inputs>
+__device__ __forceinline__ void unit_body(char *outb, Inputs in, uint32_t n, uint64_t off,
+                                          uint32_t nbytes, const uint32_t (&voff)[U]) {
+  if constexpr (ENG == kPhase)
+    chunk_body<Op, U, POL>(outb, in, n, off, nbytes, voff);
+  else
+    tile_body<Op, U, POL>(outb, in, n, off, nbytes, voff);
+}
+
 // Body inputs shifted by the head: base(k) = in[k] + head*esz.
 template <class Inner>
 struct Shifted {
@@ -342,7 +410,7 @@ struct Shifted {
 
 // ------------------------------------------------------------ kernels ------
 
-template <class Op, int BLOCK, int U, int POL>
+template <class Op, int BLOCK, int U, int POL, int ENG>
 __global__ __launch_bounds__(BLOCK) void k_reduce_single(SingleArgs a) {
   const int tid = threadIdx.x;
   uint32_t voff[U];
@@ -359,7 +427,7 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_single(SingleArgs a) {
     const uint64_t pkt0 = t * TILE;
     const uint64_t left = a.npkt - pkt0;
     const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
-    tile_body<Op, U, POL>(outb, in, a.n, pkt0 * kPacket, tile_bytes, voff);
+    unit_body<Op, U, POL, ENG>(outb, in, a.n, pkt0 * kPacket, tile_bytes, voff);
   }
 }
 
@@ -371,7 +439,7 @@ struct TableInputs {
 // All computes of a plan in one launch.  Global tile t belongs to compute c
 // with desc[c].tile_begin <= t < desc[c+1].tile_begin (desc[numdesc] is a
 // sentinel); c only grows along a workgroup's grid-stride walk.
-template <class Op, int BLOCK, int U, int POL>
+template <class Op, int BLOCK, int U, int POL, int ENG>
 __global__ __launch_bounds__(BLOCK) void k_reduce_plan(const PlanDesc *__restrict__ desc,
                                                        uint32_t c_first, uint64_t t_begin,
                                                        uint64_t t_end) {
@@ -393,7 +461,7 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_plan(const PlanDesc *__restric
     Shifted<TableInputs> in{raw, shift};
     const uint64_t left = d.npkt - pkt0;
     const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
-    tile_body<Op, U, POL>(d.out + shift, in, d.n, pkt0 * kPacket, tile_bytes, voff);
+    unit_body<Op, U, POL, ENG>(d.out + shift, in, d.n, pkt0 * kPacket, tile_bytes, voff);
   }
 }
 
@@ -560,37 +628,81 @@ int check_buffers(void *out, const void *const *in, int n, size_t count, size_t 
   return 0;
 }
 
-// Default shape, chosen from on-device sweeps ("Tuning"):
+// Engine shapes, chosen from on-device sweeps:
+//  tile   256 lanes x 4 packets (16 KiB per input per tile), for computes too
+//         small to give every CU several phased chunks;
+//  phase  512 lanes x P packets (P = 16, or 8 where the accumulator of a
+//         packet takes 8 VGPRs: bf16) -- 128 KiB per input per chunk.
+// Both: nt loads and nt stores, one workgroup per CU, grid-stride.
 constexpr int kDefBlock = 256;
 constexpr int kDefUnroll = 4;
 constexpr int kDefPol = 11;  // nt loads, nt stores
 constexpr int kDefBpc = 1;
+constexpr int kPhBlock = 512;
+// auto engine: phased when the work gives every CU at least this many chunks
+constexpr uint64_t kPhaseMinChunksPerCU = 4;
+
+// P of the phased engine: 16 packets per lane (acc + two in-flight loads =
+// 3 x 64 VGPRs at 512 lanes) unless the accumulator is wider than a packet
+// (bf16: f32x8) or the compiler reassociates the adds and holds more
+// registers (int32: exact, so it may) -- then 8.
+template <class Op>
+constexpr int phase_p() {
+  return (sizeof(typename Op::acc_t) > 16 || std::is_same<Op, OpI32>::value) ? 8 : 16;
+}
+
+int phase_p_dtype(int dtype, int acc) {
+  (void)acc;
+  return (dtype == HICCL_BFLOAT16 || dtype == HICCL_INT32) ? 8 : 16;
+}
 
 struct Cfg {
-  int block, unroll, bpc, nt, acc, grid, store;
+  int block, unroll, bpc, nt, acc, grid, store, engine;
 };
 
+// Raw config: zero block/unroll stay zero until the engine is known.
 Cfg resolve(const hiccl_reduce_config_t *c) {
-  Cfg r{kDefBlock, kDefUnroll, kDefBpc, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10};
+  Cfg r{0, 0, kDefBpc, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO};
   if (c) {
-    if (c->block) r.block = c->block;
-    if (c->unroll) r.unroll = c->unroll;
+    r.block = c->block;
+    r.unroll = c->unroll;
     if (c->blocks_per_cu) r.bpc = c->blocks_per_cu;
     if (c->nontemporal) r.nt = c->nontemporal - 1;
     r.acc = c->acc;
     r.grid = c->grid;
     if (c->store_policy) r.store = c->store_policy - 1;
+    r.engine = c->engine;
   }
   return r;
+}
+
+// Auto engine from the packets one input contributes (all computes of a launch).
+int auto_engine(uint64_t npkt, int dtype, int acc, int dev) {
+  const uint64_t chunk = (uint64_t)kPhBlock * phase_p_dtype(dtype, acc);
+  return npkt >= kPhaseMinChunksPerCU * (uint64_t)device_cus(dev) * chunk ? HICCL_ENGINE_PHASE
+                                                                           : HICCL_ENGINE_TILE;
+}
+
+// Fill in the engine and its default shape.
+void finish_cfg(Cfg &c, uint64_t npkt, int dtype, int dev) {
+  if (c.engine == HICCL_ENGINE_AUTO)
+    c.engine = (c.block || c.unroll) ? HICCL_ENGINE_TILE : auto_engine(npkt, dtype, c.acc, dev);
+  if (c.engine == HICCL_ENGINE_PHASE) {
+    if (!c.block) c.block = kPhBlock;
+    if (!c.unroll) c.unroll = phase_p_dtype(dtype, c.acc);
+  } else {
+    if (!c.block) c.block = kDefBlock;
+    if (!c.unroll) c.unroll = kDefUnroll;
+  }
 }
 
 // ---- single-compute dispatch (template instantiation table)
 
 typedef void (*single_fn)(SingleArgs, dim3, hipStream_t);
 
-template <class Op, int B, int U, int POL>
+template <class Op, int B, int U, int POL, int ENG = kTile>
 void launch_single_t(SingleArgs a, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((k_reduce_single<Op, B, U, POL>), grid, dim3(B), 0, s, a);
+  hipLaunchKernelGGL((k_reduce_single<Op, B, U, POL, ENG>), grid, dim3(B), 0, s, a);
 }
 
 template <class Op, int B, int U>
@@ -616,9 +728,41 @@ single_fn pick_u(int u, int pol) {
   }
 }
 
+// Phased engine: the default shape for every type; the headline types also
+// get the sweep shapes (chunk 64-128 KiB) and cache-policy variants.
+template <class Op, bool TUNED>
+single_fn pick_phase(const Cfg &c) {
+  constexpr int PD = phase_p<Op>();
+  const int pol = c.store * 10 + c.nt;
+  if (c.block == kPhBlock && c.unroll == PD) {
+    switch (pol) {
+      case 11: return launch_single_t<Op, kPhBlock, PD, 11, kPhase>;
+      case 1: if constexpr (TUNED) return launch_single_t<Op, kPhBlock, PD, 1, kPhase>; break;
+      case 10: if constexpr (TUNED) return launch_single_t<Op, kPhBlock, PD, 10, kPhase>; break;
+      case 21: if constexpr (TUNED) return launch_single_t<Op, kPhBlock, PD, 21, kPhase>; break;
+      case 0: if constexpr (TUNED) return launch_single_t<Op, kPhBlock, PD, 0, kPhase>; break;
+      default: break;
+    }
+    return nullptr;
+  }
+  if constexpr (TUNED) {
+    if (pol != kDefPol) return nullptr;
+    if (c.block == 1024 && c.unroll == 4) return launch_single_t<Op, 1024, 4, 11, kPhase>;
+    if constexpr (PD == 16) {
+      if (c.block == 512 && c.unroll == 8) return launch_single_t<Op, 512, 8, 11, kPhase>;
+      if (c.block == 1024 && c.unroll == 8) return launch_single_t<Op, 1024, 8, 11, kPhase>;
+      if (c.block == 256 && c.unroll == 16) return launch_single_t<Op, 256, 16, 11, kPhase>;
+    } else {
+      if (c.block == 512 && c.unroll == 4) return launch_single_t<Op, 512, 4, 11, kPhase>;
+    }
+  }
+  return nullptr;
+}
+
 // Full tuning table for the headline types; default shape for the rest.
 template <class Op, bool TUNED>
 single_fn pick_single(const Cfg &c) {
+  if (c.engine == HICCL_ENGINE_PHASE) return pick_phase<Op, TUNED>(c);
   const int pol = c.store * 10 + c.nt;
   if constexpr (TUNED) {
     if (c.block == 256) return pick_u<Op, 256>(c.unroll, pol);
@@ -644,30 +788,42 @@ single_fn pick_single_dtype(int dtype, const Cfg &c) {
   }
 }
 
-// ---- plan dispatch (default tile shape)
+// ---- plan dispatch (default shapes of the two engines)
 
 constexpr int kPlanBlock = kDefBlock;
 constexpr int kPlanUnroll = kDefUnroll;
-constexpr uint64_t kPlanTile = (uint64_t)kPlanBlock * kPlanUnroll;
 constexpr int kPlanBpc = 1;
+
+// Packets per work unit (tile or chunk) of a plan launched with `engine`.
+uint64_t unit_pkts(int engine, int dtype, int acc) {
+  return engine == HICCL_ENGINE_PHASE ? (uint64_t)kPhBlock * phase_p_dtype(dtype, acc)
+                                      : (uint64_t)kPlanBlock * kPlanUnroll;
+}
 
 typedef void (*plan_fn)(const PlanDesc *, uint32_t, uint64_t, uint64_t, dim3, hipStream_t);
 
-template <class Op>
+template <class Op, int ENG>
 void launch_plan_t(const PlanDesc *d, uint32_t c0, uint64_t t0, uint64_t t1, dim3 grid,
                    hipStream_t s) {
-  hipLaunchKernelGGL((k_reduce_plan<Op, kPlanBlock, kPlanUnroll, kDefPol>), grid, dim3(kPlanBlock), 0, s,
-                     d, c0, t0, t1);
+  constexpr int B = ENG == kPhase ? kPhBlock : kPlanBlock;
+  constexpr int U = ENG == kPhase ? phase_p<Op>() : kPlanUnroll;
+  hipLaunchKernelGGL((k_reduce_plan<Op, B, U, kDefPol, ENG>), grid, dim3(B), 0, s, d, c0, t0, t1);
 }
 
-plan_fn pick_plan(int dtype, int acc) {
+template <class Op>
+plan_fn pick_plan_eng(int engine) {
+  return engine == HICCL_ENGINE_PHASE ? launch_plan_t<Op, kPhase> : launch_plan_t<Op, kTile>;
+}
+
+plan_fn pick_plan(int dtype, int acc, int engine) {
   switch (dtype) {
-    case HICCL_FLOAT32: return launch_plan_t<OpF32>;
-    case HICCL_BFLOAT16: return acc == HICCL_ACC_WIDE ? launch_plan_t<OpBF16Wide> : launch_plan_t<OpBF16>;
-    case HICCL_FLOAT64: return launch_plan_t<OpF64>;
-    case HICCL_UINT64: return launch_plan_t<OpU64>;
-    case HICCL_INT32: return launch_plan_t<OpI32>;
-    case HICCL_BYTES: return launch_plan_t<OpRaw>;
+    case HICCL_FLOAT32: return pick_plan_eng<OpF32>(engine);
+    case HICCL_BFLOAT16:
+      return acc == HICCL_ACC_WIDE ? pick_plan_eng<OpBF16Wide>(engine) : pick_plan_eng<OpBF16>(engine);
+    case HICCL_FLOAT64: return pick_plan_eng<OpF64>(engine);
+    case HICCL_UINT64: return pick_plan_eng<OpU64>(engine);
+    case HICCL_INT32: return pick_plan_eng<OpI32>(engine);
+    case HICCL_BYTES: return pick_plan_eng<OpRaw>(engine);
     default: return nullptr;
   }
 }
@@ -679,8 +835,8 @@ uint64_t tiles_for(uint64_t npkt, uint64_t tile) {
 
 // Large-n one-shot path: stage the pointer table in stream-ordered device
 // memory and run it as a one-compute plan.
-int reduce_via_table(int dtype, int acc, void *out, const void *const *in, int n, size_t count,
-                     hipStream_t s);
+int reduce_via_table(int dtype, int acc, int engine, void *out, const void *const *in, int n,
+                     size_t count, hipStream_t s);
 
 }  // namespace
 
@@ -706,8 +862,13 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
   Cfg c = resolve(cfg);
   if (c.acc != HICCL_ACC_NATIVE && c.acc != HICCL_ACC_WIDE)
     return fail(hipErrorInvalidValue, "hiccl_reduce: bad acc mode");
+  if (c.engine < HICCL_ENGINE_AUTO || c.engine > HICCL_ENGINE_PHASE)
+    return fail(hipErrorInvalidValue, "hiccl_reduce: bad engine");
   hipStream_t s = (hipStream_t)stream;
-  if (n > kMaxArgInputs) return reduce_via_table(dtype, c.acc, out, in, n, count, s);
+  const int dev = current_device();
+  Split sp = split_on(out, count, esz);
+  finish_cfg(c, sp.npkt, dtype, dev);
+  if (n > kMaxArgInputs) return reduce_via_table(dtype, c.acc, c.engine, out, in, n, count, s);
 
   single_fn fn = pick_single_dtype(dtype, c);
   if (!fn)
@@ -715,13 +876,13 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
                                           std::to_string(c.block) + ", unroll " +
                                           std::to_string(c.unroll) + ", nt " +
                                           std::to_string(c.nt) + ", store " +
-                                          std::to_string(c.store) + ") for this dtype");
+                                          std::to_string(c.store) + ", engine " +
+                                          std::to_string(c.engine) + ") for this dtype");
   if (c.bpc < 1 || c.bpc > 64) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: blocks_per_cu");
   if (c.grid < 0) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: grid < 0");
 
   SingleArgs a;
   memset(&a, 0, sizeof(a));
-  Split sp = split_on(out, count, esz);
   a.out = (char *)out;
   a.npkt = sp.npkt;
   a.head = sp.head;
@@ -731,7 +892,6 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
   a.ntiles = tiles_for(sp.npkt, tile);
   for (int k = 0; k < n; k++) a.in[k] = (const char *)in[k];
 
-  const int dev = current_device();
   uint64_t grid = c.grid > 0 ? (uint64_t)c.grid : (uint64_t)device_cus(dev) * c.bpc;
   if (grid > a.ntiles) grid = a.ntiles;
   fn(a, dim3((unsigned)grid), s);
@@ -759,6 +919,8 @@ struct hiccl_reduce_plan {
   int dtype = 0;
   int device = 0;
   int acc = HICCL_ACC_NATIVE;
+  int engine_req = HICCL_ENGINE_AUTO;  // hiccl_reduce_plan_set_engine
+  int engine = HICCL_ENGINE_TILE;      // resolved at upload
   size_t esz = 0;
   struct Comp {
     void *out;
@@ -796,6 +958,11 @@ int plan_upload(hiccl_reduce_plan *p) {
                                   hipMemcpyHostToDevice), "plan: upload ptrs"))
     return e;
   p->host_desc.assign(nc + 1, PlanDesc{});
+  uint64_t total_pkt = 0;
+  for (auto &c : p->comps) total_pkt += split_on(c.out, c.count, p->esz).npkt;
+  p->engine = p->engine_req != HICCL_ENGINE_AUTO ? p->engine_req
+                                                 : auto_engine(total_pkt, p->dtype, p->acc, p->device);
+  const uint64_t unit = unit_pkts(p->engine, p->dtype, p->acc);
   uint64_t tile = 0;
   size_t off = 0;
   p->maxn = 0;
@@ -810,7 +977,7 @@ int plan_upload(hiccl_reduce_plan *p) {
     d.tail = sp.tail;
     d.n = (uint32_t)c.in.size();
     d.tile_begin = tile;
-    tile += tiles_for(sp.npkt, kPlanTile);
+    tile += tiles_for(sp.npkt, unit);
     off += c.in.size();
     if ((int)c.in.size() > p->maxn) p->maxn = (int)c.in.size();
   }
@@ -827,7 +994,7 @@ int plan_upload(hiccl_reduce_plan *p) {
 
 int plan_kernel(hiccl_reduce_plan *p, uint32_t c0, uint64_t t0, uint64_t t1, int maxn,
                 hipStream_t s) {
-  plan_fn fn = pick_plan(p->dtype, p->acc);
+  plan_fn fn = pick_plan(p->dtype, p->acc, p->engine);
   if (!fn) return fail(hipErrorInvalidValue, "plan: unsupported dtype");
   uint64_t grid = (uint64_t)device_cus(p->device) * kPlanBpc;
   if (grid > t1 - t0) grid = t1 - t0;
@@ -835,8 +1002,8 @@ int plan_kernel(hiccl_reduce_plan *p, uint32_t c0, uint64_t t0, uint64_t t1, int
   return check_hip(hipGetLastError(), "plan: launch");
 }
 
-int reduce_via_table(int dtype, int acc, void *out, const void *const *in, int n, size_t count,
-                     hipStream_t s) {
+int reduce_via_table(int dtype, int acc, int engine, void *out, const void *const *in, int n,
+                     size_t count, hipStream_t s) {
   const size_t esz = esize(dtype);
   Split sp = split_on(out, count, esz);
   const size_t bytes = 2 * sizeof(PlanDesc) + (size_t)n * sizeof(void *);
@@ -854,12 +1021,12 @@ int reduce_via_table(int dtype, int acc, void *out, const void *const *in, int n
   hd[0].tail = sp.tail;
   hd[0].n = (uint32_t)n;
   hd[0].tile_begin = 0;
-  const uint64_t tiles = tiles_for(sp.npkt, kPlanTile);
+  const uint64_t tiles = tiles_for(sp.npkt, unit_pkts(engine, dtype, acc));
   hd[1].tile_begin = UINT64_MAX;
   if (int e = check_hip(hipMemcpyAsync(dmem, host.data(), bytes, hipMemcpyHostToDevice, s),
                         "hiccl_reduce: table upload"))
     return e;
-  plan_fn fn = pick_plan(dtype, acc);
+  plan_fn fn = pick_plan(dtype, acc, engine);
   uint64_t grid = (uint64_t)device_cus(current_device()) * kPlanBpc;
   if (grid > tiles) grid = tiles;
   fn((const PlanDesc *)dmem, 0, 0, tiles, dim3((unsigned)grid), s);
@@ -898,8 +1065,20 @@ int hiccl_reduce_plan_set_acc(hiccl_reduce_plan_t *p, int acc) {
   if (acc != HICCL_ACC_NATIVE && acc != HICCL_ACC_WIDE)
     return fail(hipErrorInvalidValue, "plan_set_acc: bad mode");
   p->acc = acc;
+  p->dirty = true;  // the auto engine's chunk size depends on the accumulator
   return 0;
 }
+
+int hiccl_reduce_plan_set_engine(hiccl_reduce_plan_t *p, int engine) {
+  if (!p) return fail(hipErrorInvalidValue, "plan_set_engine: plan is NULL");
+  if (engine < HICCL_ENGINE_AUTO || engine > HICCL_ENGINE_PHASE)
+    return fail(hipErrorInvalidValue, "plan_set_engine: bad engine");
+  p->engine_req = engine;
+  p->dirty = true;
+  return 0;
+}
+
+int hiccl_reduce_plan_engine(const hiccl_reduce_plan_t *p) { return p ? p->engine : -1; }
 
 int hiccl_reduce_plan_add(hiccl_reduce_plan_t *p, void *out, const void *const *in, int n,
                           size_t count) {
@@ -931,15 +1110,17 @@ int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *p, void *stream) {
   if (!p) return fail(hipErrorInvalidValue, "plan_launch_each: plan is NULL");
   if (int e = check_hip(hipSetDevice(p->device), "plan_launch_each: hipSetDevice")) return e;
   if (p->comps.empty()) return 0;
-  if (int e = plan_upload(p)) return e;
-  hipStream_t s = (hipStream_t)stream;
-  for (size_t c = 0; c < p->comps.size(); c++) {
-    const uint64_t t0 = p->host_desc[c].tile_begin;
-    const uint64_t t1 = (c + 1 < p->comps.size()) ? p->host_desc[c + 1].tile_begin : p->total_tiles;
-    if (int e = plan_kernel(p, (uint32_t)c, t0, t1, (int)p->comps[c].in.size(), s)) return e;
-  }
+  // One one-shot launch per compute, each with the engine AUTO picks for that
+  // compute alone (the reference's structure, compute.h:141-145).
+  hiccl_reduce_config_t cfg;
+  memset(&cfg, 0, sizeof(cfg));
+  cfg.acc = p->acc;
+  cfg.engine = p->engine_req;
+  for (auto &c : p->comps)
+    if (int e = hiccl_reduce_ex(p->dtype, c.out, c.in.data(), (int)c.in.size(), c.count, stream, &cfg))
+      return e;
   p->launched = true;
-  return check_hip(hipEventRecord(p->done, s), "plan_launch_each: event");
+  return check_hip(hipEventRecord(p->done, (hipStream_t)stream), "plan_launch_each: event");
 }
 
 int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *p) {

@@ -49,6 +49,20 @@ typedef enum {
   HICCL_ACC_WIDE = 1    /* accumulate bf16 in f32, round once: NOT reference-bitwise */
 } hiccl_acc_t;
 
+/* Kernel engine (both compute the same bits; they differ in access order).
+ *   TILE   all n inputs of a 16 KiB-per-input tile are loaded together;
+ *          suits computes too small to give every CU several chunks.
+ *   PHASE  a workgroup sweeps a 128 KiB chunk of input 0, then of input 1,
+ *          ... (next input's loads in flight while the current one is
+ *          added), then writes the chunk: only ~2 input streams are open
+ *          chip-wide at a time.  Default for large buckets.
+ *   AUTO   PHASE when every CU gets >= 4 chunks, else TILE. */
+typedef enum {
+  HICCL_ENGINE_AUTO = 0,
+  HICCL_ENGINE_TILE = 1,
+  HICCL_ENGINE_PHASE = 2
+} hiccl_engine_t;
+
 /* Size in bytes of one element of `dtype`, 0 if unknown. */
 size_t hiccl_dtype_size(int dtype);
 
@@ -79,15 +93,18 @@ int hiccl_reduce_f32(float *out, const float *const *in, int n, size_t count, vo
 int hiccl_reduce_bf16(uint16_t *out, const uint16_t *const *in, int n, size_t count,
                       void *stream);
 
-/* Tuning knobs of the single-compute kernel.  Zero fields mean "default". */
+/* Tuning knobs of the single-compute kernel.  Zero fields mean "default".
+ * With engine AUTO, a non-zero block or unroll selects the TILE engine. */
 typedef struct {
-  int block;         /* threads per workgroup: 256 or 512 */
-  int unroll;        /* 16-byte packets per input per lane per tile: 1, 2 or 4 */
+  int block;         /* threads per workgroup: TILE 256 or 512; PHASE 256, 512 or 1024 */
+  int unroll;        /* 16-byte packets per input per lane per tile: TILE 1, 2 or 4;
+                        PHASE 4, 8 or 16 (chunk = block * unroll * 16 B) */
   int blocks_per_cu; /* persistent grid = CUs x this (capped by tiles) */
   int nontemporal;   /* loads: 1 plain cache policy, 2 nt */
   int acc;           /* hiccl_acc_t */
   int grid;          /* total workgroups; overrides blocks_per_cu when > 0 */
   int store_policy;  /* stores: 1 plain, 2 nt, 3 sc1 (write-through, line dropped from L2) */
+  int engine;        /* hiccl_engine_t */
 } hiccl_reduce_config_t;
 
 int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t count,
@@ -122,11 +139,18 @@ typedef struct hiccl_reduce_plan hiccl_reduce_plan_t;
 
 int hiccl_reduce_plan_create(hiccl_reduce_plan_t **plan, int dtype, int device);
 int hiccl_reduce_plan_set_acc(hiccl_reduce_plan_t *plan, int acc);
+/* Engine for the plan's launches (hiccl_engine_t; default AUTO, decided from
+ * the total packets of all computes at the first launch after an add). */
+int hiccl_reduce_plan_set_engine(hiccl_reduce_plan_t *plan, int engine);
+/* The engine the last upload resolved to (TILE before the first launch). */
+int hiccl_reduce_plan_engine(const hiccl_reduce_plan_t *plan);
 int hiccl_reduce_plan_add(hiccl_reduce_plan_t *plan, void *out, const void *const *in, int n,
                           size_t count);
 int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *plan, void *stream);
 /* Reference structure, for measurement: one kernel per compute, each on
- * the given stream (compute.h:141-145 launches one kernel per compute). */
+ * the given stream (compute.h:141-145 launches one kernel per compute) --
+ * each one a one-shot hiccl_reduce_ex with the plan's acc and engine
+ * request (AUTO decides per compute). */
 int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *plan, void *stream);
 int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *plan);
 /* The plan's own non-blocking stream (a hipStream_t), created on the first

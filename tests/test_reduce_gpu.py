@@ -18,6 +18,10 @@ from conftest import bits_equal, first_mismatch, load_golden
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
+# Both kernel engines compute the same bits; every edge-case test runs under
+# the default (auto: tile for these small sizes) and the forced phased engine.
+PHASE = dict(engine=hiccl_amd.HICCL_ENGINE_PHASE)
+ENGINES = pytest.mark.parametrize("eng", [None, PHASE], ids=["auto", "phase"])
 TORCH_OF = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
             np.dtype(np.uint64): torch.int64, np.dtype(np.uint16): torch.bfloat16}
 
@@ -68,49 +72,95 @@ def gpu_reduce(x, count, dtype, offsets=None, out_offset=0, config=None):
 
 @pytest.mark.parametrize("name,dtype", [("reduce_f32", np.float32), ("reduce_f64", np.float64),
                                         ("reduce_u64", np.uint64), ("reduce_bf16", np.uint16)])
-def test_golden_fixtures(name, dtype):
+@ENGINES
+def test_golden_fixtures(name, dtype, eng):
     for case, d in load_golden(name).items():
         x, y = d["in"], d["out"]
-        got = gpu_reduce(x, len(y), dtype)
+        got = gpu_reduce(x, len(y), dtype, config=eng)
         assert bits_equal(got, y), f"{name}/{case}: {first_mismatch(got, y)}"
 
 
 @pytest.mark.parametrize("offs", [[1, 0], [0, 3], [1, 2, 3, 0], [3, 3, 3], [2, 1, 0, 3, 2, 1, 0, 3, 1]])
 @pytest.mark.parametrize("out_off", [0, 1, 3])
-def test_misaligned_inputs_f32(oracle, offs, out_off):
+@ENGINES
+def test_misaligned_inputs_f32(oracle, offs, out_off, eng):
     n = len(offs)
     for count in (1, 5, 4099, 70001):
         x = oracle.fill(n, count, seed=11 + count)
-        got = gpu_reduce(x, count, np.float32, offsets=offs, out_offset=out_off)
+        got = gpu_reduce(x, count, np.float32, offsets=offs, out_offset=out_off, config=eng)
         exp = oracle.reduce(list(x))
         assert bits_equal(got, exp), f"offs={offs} out={out_off} count={count}: {first_mismatch(got, exp)}"
 
 
 @pytest.mark.parametrize("offs", [[1, 0, 5], [7, 3], [0, 0, 1, 2, 3, 4, 5, 6]])
-def test_misaligned_inputs_bf16(oracle, offs):
+@ENGINES
+def test_misaligned_inputs_bf16(oracle, offs, eng):
     n = len(offs)
     for count in (3, 9, 4099, 33333):
         x = oracle.fill(n, count, seed=5, dtype=np.uint16)
-        got = gpu_reduce(x, count, np.uint16, offsets=offs, out_offset=1)
+        got = gpu_reduce(x, count, np.uint16, offsets=offs, out_offset=1, config=eng)
         exp = oracle.reduce(list(x), dtype=np.uint16)
         assert bits_equal(got, exp), f"offs={offs} count={count}: {first_mismatch(got, exp)}"
 
 
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 5, 6, 7, 8, 9, 15, 16, 17, 31, 64, 65, 100, 200])
-def test_input_counts(oracle, n):
+@ENGINES
+def test_input_counts(oracle, n, eng):
     count = 3 * 4096 + 77
     x = oracle.fill(n, count, seed=n) if n else np.zeros((0, count), np.float32)
-    got = gpu_reduce(x, count, np.float32)
+    got = gpu_reduce(x, count, np.float32, config=eng)
     exp = oracle.reduce(list(x), count=count, dtype=np.float32)
     assert bits_equal(got, exp), f"n={n}: {first_mismatch(got, exp)}"
 
 
 @pytest.mark.parametrize("count", [1, 2, 3, 4, 5, 511, 512, 513, 2047, 2048, 2049, 8191, 8192, 8193,
                                    131072 * 4 + 3])
-def test_tile_boundaries(oracle, count):
+@ENGINES
+def test_tile_boundaries(oracle, count, eng):
     x = oracle.fill(4, count, seed=3)
-    got = gpu_reduce(x, count, np.float32)
+    got = gpu_reduce(x, count, np.float32, config=eng)
     assert bits_equal(got, oracle.reduce(list(x)))
+
+
+@pytest.mark.parametrize("count", [8192 * 4 - 1, 8192 * 4, 8192 * 4 + 1, 8192 * 4 * 3 + 5,
+                                   32768 * 4 * 2 + 4 * 1000 + 3])
+@pytest.mark.parametrize("n", [1, 2, 7, 8])
+def test_phase_chunk_boundaries(oracle, count, n):
+    """Phased chunks are 512 x 16 packets (f32: 32768 elements; bf16 8
+    packets: 32768 elements): partial last chunks, odd/even n."""
+    x = oracle.fill(n, count, seed=count + n)
+    got = gpu_reduce(x, count, np.float32, offsets=[1] + [0] * (n - 1), config=PHASE)
+    assert bits_equal(got, oracle.reduce(list(x)))
+    xb = oracle.fill(n, count, seed=count, dtype=np.uint16)
+    gotb = gpu_reduce(xb, count, np.uint16, config=PHASE)
+    assert bits_equal(gotb, oracle.reduce(list(xb), dtype=np.uint16))
+
+
+@pytest.mark.parametrize("config", [
+    dict(engine=2), dict(engine=2, block=1024, unroll=4), dict(engine=2, block=512, unroll=8),
+    dict(engine=2, block=1024, unroll=8), dict(engine=2, block=256, unroll=16),
+    dict(engine=2, nontemporal=1, store_policy=1), dict(engine=2, nontemporal=2, store_policy=3),
+    dict(engine=2, nontemporal=1), dict(engine=2, grid=5), dict(engine=2, blocks_per_cu=2)])
+def test_phase_variants_same_bits(oracle, config):
+    """Every instantiated phased shape / cache policy gives the reference bits
+    (f32; bf16 where the shape exists for bf16)."""
+    bf16_ok = (config.get("block", 512), config.get("unroll", 8)) in ((512, 8), (1024, 4), (512, 4))
+    for n, count in ((8, (1 << 20) + 3), (3, 123457), (1, 77777)):
+        x = oracle.fill(n, count, seed=n)
+        got = gpu_reduce(x, count, np.float32, offsets=[0, 1, 2][:n] + [0] * (n - 3), config=config)
+        assert bits_equal(got, oracle.reduce(list(x))), config
+        if bf16_ok:
+            xb = oracle.fill(n, count, seed=n, dtype=np.uint16)
+            gotb = gpu_reduce(xb, count, np.uint16, config=config)
+            assert bits_equal(gotb, oracle.reduce(list(xb), dtype=np.uint16)), config
+
+
+def test_phase_unsupported_shape_is_an_error():
+    x = torch.zeros(100, device=DEV)
+    with pytest.raises(hiccl_amd.HicclError):
+        hiccl_amd.reduce(x, [x, x], config=dict(engine=2, block=128, unroll=16))
+    with pytest.raises(hiccl_amd.HicclError):
+        hiccl_amd.reduce(x, [x, x], config=dict(engine=7))
 
 
 @pytest.mark.parametrize("config", [
@@ -130,40 +180,44 @@ def test_tuning_variants_same_bits(oracle, config):
         assert bits_equal(gotb, oracle.reduce(list(xb), dtype=np.uint16)), config
 
 
-def test_in_place_output(oracle):
+@ENGINES
+def test_in_place_output(oracle, eng):
     n, count = 4, 100003
     x = oracle.fill(n, count, seed=9)
     ins = [to_dev(r) for r in x]
     for k in range(n):  # out aliases input k exactly
         t = [i.clone() for i in ins]
-        hiccl_amd.reduce(t[k], t, count=count)
+        hiccl_amd.reduce(t[k], t, count=count, config=eng)
         torch.cuda.synchronize()
         assert bits_equal(t[k].cpu().numpy(), oracle.reduce(list(x))), k
 
 
-def test_in_place_large_n_table_path(oracle):
+@ENGINES
+def test_in_place_large_n_table_path(oracle, eng):
     n, count = 80, 20011
     x = oracle.fill(n, count, seed=1)
     t = [to_dev(r) for r in x]
-    hiccl_amd.reduce(t[70], t, count=count)
+    hiccl_amd.reduce(t[70], t, count=count, config=eng)
     torch.cuda.synchronize()
     assert bits_equal(t[70].cpu().numpy(), oracle.reduce(list(x)))
 
 
-def test_bf16_wide_accumulation(oracle):
+@ENGINES
+def test_bf16_wide_accumulation(oracle, eng):
     n, count = 8, 50001
     x = oracle.fill(n, count, seed=2, dtype=np.uint16)
-    got = gpu_reduce(x, count, np.uint16, config=dict(acc=hiccl_amd.HICCL_ACC_WIDE))
+    got = gpu_reduce(x, count, np.uint16, config=dict(acc=hiccl_amd.HICCL_ACC_WIDE, **(eng or {})))
     exp = oracle.reduce(list(x), dtype=np.uint16, wide=True)
     assert bits_equal(got, exp), first_mismatch(got, exp)
 
 
-def test_int32_wraparound(oracle):
+@ENGINES
+def test_int32_wraparound(oracle, eng):
     rng = np.random.default_rng(0)
     x = rng.integers(-2**31, 2**31 - 1, size=(5, 10007), dtype=np.int64).astype(np.int32)
     ins = [torch.from_numpy(r.copy()).to(DEV) for r in x]
     out = torch.empty(10007, dtype=torch.int32, device=DEV)
-    hiccl_amd.reduce(out, ins)
+    hiccl_amd.reduce(out, ins, config=eng)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), oracle.reduce(list(x)))
 
@@ -177,9 +231,9 @@ def test_generator_matches_oracle(oracle):
         assert bits_equal(to_host(t, dtype), exp), dtype
 
 
-def _plan_case(oracle, each):
+def _plan_case(oracle, each, engine=hiccl_amd.HICCL_ENGINE_AUTO):
     rng = np.random.default_rng(4)
-    comp = hiccl_amd.Compute(torch.float32, device=0)
+    comp = hiccl_amd.Compute(torch.float32, device=0, engine=engine)
     expected = []
     outs = []
     keep = []
@@ -202,6 +256,8 @@ def _plan_case(oracle, each):
     assert comp.numcomp == 37
     comp.start(each=each)
     comp.wait()
+    if not each:  # launch_each runs one-shot launches and leaves the plan's table alone
+        assert comp.engine() == (hiccl_amd.HICCL_ENGINE_TILE if engine == hiccl_amd.HICCL_ENGINE_AUTO else engine)
     for (ob, count), exp in zip(outs, expected):
         got = ob[1:1 + count].cpu().numpy()
         assert bits_equal(got, exp), first_mismatch(got, exp)
@@ -221,6 +277,32 @@ def test_plan_launch_each(oracle):
     _plan_case(oracle, each=True)
 
 
+@pytest.mark.parametrize("each", [False, True])
+def test_plan_phase_engine(oracle, each):
+    _plan_case(oracle, each=each, engine=hiccl_amd.HICCL_ENGINE_PHASE)
+
+
+def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
+    """AUTO resolves to PHASE once every CU gets >= 4 chunks of 128 KiB
+    (f32: 2^25 elements per input on 256 CUs), to TILE below."""
+    count = 1 << 25
+    a = torch.empty(count, device=DEV)
+    hiccl_amd.fill_uniform(a, 77, 0)
+    out = torch.empty(count, device=DEV)
+    for cnt, expect in ((count, hiccl_amd.HICCL_ENGINE_PHASE), (1 << 20, hiccl_amd.HICCL_ENGINE_TILE)):
+        comp = hiccl_amd.Compute(torch.float32, device=0)
+        comp.add([a, a], out, cnt, compid=0)
+        comp.start()
+        comp.wait()
+        if torch.cuda.get_device_properties(0).multi_processor_count == 256:
+            assert comp.engine() == expect
+        idx = np.array([0, 1, cnt // 2, cnt - 1], np.int64)
+        exp = oracle.sample_sum(idx.astype(np.uint64), 77, 1)
+        got = out[torch.from_numpy(idx).to(DEV)].cpu().numpy()
+        assert bits_equal(got, (exp + exp).astype(np.float32))
+        comp.close()
+
+
 def test_plan_launch_from_other_thread(oracle):
     """Comm::start runs compute->start() on a pthread (comm.h:214-224)."""
     import threading
@@ -236,7 +318,8 @@ def test_plan_launch_from_other_thread(oracle):
 
 
 @pytest.mark.parametrize("count", [1 << 28, 250_000_000], ids=["2^28", "readme_2.5e8"])
-def test_full_size_sampled(oracle, count):
+@pytest.mark.parametrize("eng", [None, dict(engine=hiccl_amd.HICCL_ENGINE_TILE)], ids=["auto", "tile"])
+def test_full_size_sampled(oracle, count, eng):
     """Config 2 shape (8 x 2^28 f32, and the README's 1e9/sizeof(float)
     count for tail handling) checked at 4096 random indices plus the ends: a
     size-independent property check against the oracle's generator."""
@@ -248,7 +331,7 @@ def test_full_size_sampled(oracle, count):
     for k, t in enumerate(ins):
         hiccl_amd.fill_uniform(t, seed, k)
     out = torch.empty(count, device=DEV)
-    hiccl_amd.reduce(out, ins)
+    hiccl_amd.reduce(out, ins, config=eng)
     torch.cuda.synchronize()
     rng = np.random.default_rng(0)
     idx = np.concatenate([np.arange(64), count - 64 + np.arange(64),
@@ -265,7 +348,8 @@ def test_full_size_sampled(oracle, count):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.uint16])
-def test_plan_partitioned_on_default_stream(oracle, dtype):
+@pytest.mark.parametrize("engine", [hiccl_amd.HICCL_ENGINE_AUTO, hiccl_amd.HICCL_ENGINE_PHASE])
+def test_plan_partitioned_on_default_stream(oracle, dtype, engine):
     """Config-4 layout: one bucket split into pipedepth computes with the
     partition() formula (reduce.h:401-415: count/numbatch + (b < count%numbatch)),
     launched as ONE batched kernel on torch's (NULL) default stream."""
@@ -274,7 +358,7 @@ def test_plan_partitioned_on_default_stream(oracle, dtype):
     x = oracle.fill(n, count, seed=21, dtype=dtype)
     ins = [to_dev(r).view(tdt) for r in x]
     out = torch.full((count,), 7.0, dtype=tdt, device=DEV)
-    comp = hiccl_amd.Compute(tdt, device=0)
+    comp = hiccl_amd.Compute(tdt, device=0, engine=engine)
     off = 0
     for b in range(depth):
         c = count // depth + (1 if b < count % depth else 0)

@@ -1,0 +1,271 @@
+// tools/phase_probe.hip -- bench-only probes (not part of the product).
+//
+// Question: the 8-read + 1-write reduction runs at 5.5-5.65 TB/s or at
+// 6.1-6.3 TB/s depending on the physical placement of the nine 1 GiB
+// buckets (profiles/r01_placement.txt).  A placement effect of that kind is
+// what DRAM bank/row conflicts between streams look like: the product kernel
+// keeps all nine streams open at the same element offset at the same time.
+// These probes change WHICH streams are open at once:
+//
+//   k_phase<B,P>  input-phased: a workgroup owns a chunk of B*P packets; it
+//                 sweeps input 0 of the chunk, then input 1, ... (register
+//                 accumulators, next input's loads in flight while the
+//                 current one is added), then stores the chunk.  Chip-wide
+//                 only ~1-2 input streams are open at any moment.
+//   k_slab<B,U>   the product's tile order, but each workgroup walks its
+//                 own contiguous slab instead of grid-striding.
+//
+// Plus allocation modes for the placement itself (hipMalloc, contiguous
+// hipExtMallocWithFlags, VMM physical handles mapped into one range).
+//
+// Sums are f32 in input order starting from +0: bit-identical to the
+// reference's reduce_kernel (source/compute.h:2-12) whatever the order of
+// the loop nest, since each element's additions are still in input order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t mk(const void *p, uint32_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc((void *)p, (short)0, (int)n, 0x00020000);
+}
+
+struct PArgs {
+  const char *in[16];
+  char *out;
+  uint64_t bytes;  // per stream, multiple of 16
+  int n;
+};
+
+template <int AUX>
+__device__ __forceinline__ f32x4 ld(rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, AUX));
+}
+
+// Input-phased chunk sweep.
+template <int B, int P, int AUXL, int AUXS>
+__global__ __launch_bounds__(B) void k_phase(PArgs a) {
+  constexpr uint64_t CH = (uint64_t)B * P * 16;
+  const uint64_t nch = (a.bytes + CH - 1) / CH;
+  uint32_t voff[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) voff[p] = (uint32_t)((p * B + threadIdx.x) * 16);
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    const uint64_t off = c * CH;
+    const uint32_t nb = (uint32_t)((a.bytes - off) < CH ? (a.bytes - off) : CH);
+    f32x4 acc[P], x[P], y[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) acc[p] = (f32x4)(0.0f);
+    rsrc_t r = mk(a.in[0] + off, nb);
+#pragma unroll
+    for (int p = 0; p < P; p++) x[p] = ld<AUXL>(r, voff[p]);
+    int j = 0;
+    for (; j + 2 <= a.n; j += 2) {  // x holds input j (in flight)
+      rsrc_t ry = mk(a.in[j + 1] + off, nb);
+#pragma unroll
+      for (int p = 0; p < P; p++) y[p] = ld<AUXL>(ry, voff[p]);
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] += x[p];
+      if (j + 2 < a.n) {
+        rsrc_t rx = mk(a.in[j + 2] + off, nb);
+#pragma unroll
+        for (int p = 0; p < P; p++) x[p] = ld<AUXL>(rx, voff[p]);
+      }
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] += y[p];
+    }
+    if (j < a.n) {
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] += x[p];
+    }
+    rsrc_t w = mk(a.out + off, nb);
+#pragma unroll
+    for (int p = 0; p < P; p++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[p]), w, (int)voff[p], 0, AUXS);
+  }
+}
+
+// Input-phased, N static, D input stages in flight: input j+D-1's loads are
+// issued before input j's adds; sched_barriers keep the scheduler from
+// hoisting later inputs.
+template <int B, int P, int N, int D, int AUXL, int AUXS>
+__global__ __launch_bounds__(B) void k_phase_n(PArgs a) {
+  constexpr uint64_t CH = (uint64_t)B * P * 16;
+  const uint64_t nch = (a.bytes + CH - 1) / CH;
+  uint32_t voff[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) voff[p] = (uint32_t)((p * B + threadIdx.x) * 16);
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    const uint64_t off = c * CH;
+    const uint32_t nb = (uint32_t)((a.bytes - off) < CH ? (a.bytes - off) : CH);
+    f32x4 acc[P], x[D][P];
+#pragma unroll
+    for (int p = 0; p < P; p++) acc[p] = (f32x4)(0.0f);
+#pragma unroll
+    for (int j = 0; j < D - 1 && j < N; j++) {
+      rsrc_t r = mk(a.in[j] + off, nb);
+#pragma unroll
+      for (int p = 0; p < P; p++) x[j % D][p] = ld<AUXL>(r, voff[p]);
+    }
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      if (j + D - 1 < N) {
+        rsrc_t r = mk(a.in[j + D - 1] + off, nb);
+#pragma unroll
+        for (int p = 0; p < P; p++) x[(j + D - 1) % D][p] = ld<AUXL>(r, voff[p]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] += x[j % D][p];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    rsrc_t w = mk(a.out + off, nb);
+#pragma unroll
+    for (int p = 0; p < P; p++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[p]), w, (int)voff[p], 0, AUXS);
+  }
+}
+
+// Product tile order (all n inputs of a tile loaded together), slab-walked.
+template <int B, int U, int AUXL, int AUXS>
+__global__ __launch_bounds__(B) void k_slab(PArgs a) {
+  constexpr uint64_t TILE = (uint64_t)B * U * 16;
+  const uint64_t nt = (a.bytes + TILE - 1) / TILE;
+  const uint64_t per = (nt + gridDim.x - 1) / gridDim.x;
+  const uint64_t t0 = blockIdx.x * per, t1 = (t0 + per < nt) ? t0 + per : nt;
+  uint32_t voff[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * B + threadIdx.x) * 16);
+  for (uint64_t t = t0; t < t1; t++) {
+    const uint64_t off = t * TILE;
+    const uint32_t nb = (uint32_t)((a.bytes - off) < TILE ? (a.bytes - off) : TILE);
+    f32x4 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) acc[u] = (f32x4)(0.0f);
+    for (int g = 0; g < a.n; g += 8) {
+      f32x4 x[8][U];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        rsrc_t r = mk(a.in[g + j < a.n ? g + j : 0] + off, g + j < a.n ? nb : 0u);
+#pragma unroll
+        for (int u = 0; u < U; u++) x[j][u] = ld<AUXL>(r, voff[u]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        if (g + j < a.n)
+#pragma unroll
+          for (int u = 0; u < U; u++) acc[u] += x[j][u];
+    }
+    rsrc_t w = mk(a.out + off, nb);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[u]), w, (int)voff[u], 0, AUXS);
+  }
+}
+
+template <class K>
+static int launch(K k, int grid, int block, const PArgs &a, hipStream_t s) {
+  hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" {
+
+// kind 0: phase, kind 1: slab.  param = P (phase) or U (slab).
+int pp_run(int kind, int block, int param, int depth, int nt, int grid, const void *const *in, int n,
+           void *out, uint64_t bytes, void *stream) {
+  if (n < 1 || n > 16 || (bytes & 15)) return -2;
+  PArgs a;
+  for (int k = 0; k < 16; k++) a.in[k] = (const char *)(k < n ? in[k] : in[0]);
+  a.out = (char *)out;
+  a.bytes = bytes;
+  a.n = n;
+  hipStream_t s = (hipStream_t)stream;
+#define PH(B, P)                                                                        \
+  if (block == B && param == P)                                                          \
+    return nt ? launch(k_phase<B, P, 2, 2>, grid, B, a, s) : launch(k_phase<B, P, 0, 0>, grid, B, a, s);
+#define SL(B, U)                                                                        \
+  if (block == B && param == U)                                                          \
+    return nt ? launch(k_slab<B, U, 2, 2>, grid, B, a, s) : launch(k_slab<B, U, 0, 0>, grid, B, a, s);
+#define PN(B, P, D)                                                                     \
+  if (block == B && param == P && depth == D)                                            \
+    return nt ? launch(k_phase_n<B, P, 8, D, 2, 2>, grid, B, a, s)                       \
+              : launch(k_phase_n<B, P, 8, D, 0, 0>, grid, B, a, s);
+  if (kind == 0) {
+    PH(256, 4) PH(256, 8) PH(256, 16) PH(256, 32) PH(512, 8) PH(512, 16) PH(1024, 4) PH(1024, 8)
+  } else if (kind == 2) {
+    if (n != 8) return -3;
+    PN(256, 8, 2) PN(256, 16, 2) PN(512, 8, 2) PN(1024, 4, 2) PN(1024, 8, 2)
+    PN(512, 8, 3) PN(1024, 4, 3) PN(512, 4, 3) PN(512, 4, 4) PN(1024, 8, 3) PN(256, 16, 3)
+    PN(512, 16, 2)
+  } else {
+    SL(256, 4) SL(256, 2) SL(512, 4)
+  }
+#undef PH
+#undef SL
+  return -1;
+}
+
+// Allocation modes: 0 hipMalloc, 1 hipExtMallocWithFlags(contiguous),
+// 2 VMM (hipMemCreate physical handle, reserved + mapped + RW access).
+int pp_alloc(void **p, uint64_t bytes, int mode) {
+  if (mode == 0) return (int)hipMalloc(p, bytes);
+  if (mode == 1) return (int)hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
+  if (mode == 2) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    size_t gran = 0;
+    hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+    if (e) return (int)e;
+    bytes = (bytes + gran - 1) / gran * gran;
+    hipMemGenericAllocationHandle_t h;
+    if ((e = hipMemCreate(&h, bytes, &prop, 0))) return (int)e;
+    void *va = nullptr;
+    if ((e = hipMemAddressReserve(&va, bytes, 0, nullptr, 0))) return (int)e;
+    if ((e = hipMemMap(va, bytes, 0, h, 0))) return (int)e;
+    hipMemAccessDesc d = {};
+    d.location = prop.location;
+    d.flags = hipMemAccessFlagsProtReadWrite;
+    if ((e = hipMemSetAccess(va, bytes, &d, 1))) return (int)e;
+    *p = va;
+    return 0;
+  }
+  return -1;
+}
+
+uint64_t pp_granularity(void) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  size_t g0 = 0, g1 = 0;
+  hipMemGetAllocationGranularity(&g0, &prop, hipMemAllocationGranularityMinimum);
+  hipMemGetAllocationGranularity(&g1, &prop, hipMemAllocationGranularityRecommended);
+  return (g0 << 32) | (g1 & 0xffffffffu);
+}
+}
+
+__global__ void k_diff(const uint32_t *a, const uint32_t *b, uint64_t nw, unsigned long long *cnt) {
+  unsigned long long c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x)
+    c += (a[i] != b[i]);
+  if (c) atomicAdd(cnt, c);
+}
+
+extern "C" long long pp_diff(const void *a, const void *b, uint64_t bytes) {
+  unsigned long long *d = nullptr, h = 0;
+  if (hipMalloc(&d, 8)) return -1;
+  hipMemset(d, 0, 8);
+  hipLaunchKernelGGL(k_diff, dim3(2048), dim3(256), 0, 0, (const uint32_t *)a, (const uint32_t *)b, bytes / 4, d);
+  hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
+  hipFree(d);
+  return (long long)h;
+}
