@@ -263,8 +263,14 @@ def sample_check(out, n, count, bf16=False, seed=SEED, nsample=1024):
     return bool(np.array_equal(got.view(np.uint8), exp.view(np.uint8)))
 
 
-def traffic_from_profiles(n, count):
-    """HBM bytes per launch from a committed PMC summary for this workload."""
+# The kernel the default (auto) config runs on C2: the phased engine's f32
+# default shape (hiccl_amd/csrc/reduce.hip: 512 lanes x 16 packets, nt/nt).
+DEFAULT_KERNEL = "OpF32, 512, 16, 11, 1>"
+
+
+def traffic_from_profiles(n, count, kernel=DEFAULT_KERNEL):
+    """HBM bytes per launch from a committed PMC summary of this workload AND
+    this kernel (profiles/*_pmc.json written by tools/profile.sh)."""
     pdir = os.path.join(ROOT, "profiles")
     best = None
     if not os.path.isdir(pdir):
@@ -275,7 +281,8 @@ def traffic_from_profiles(n, count):
                 d = json.load(open(os.path.join(pdir, f)))
             except (OSError, ValueError):
                 continue
-            if d.get("n_inputs") == n and d.get("count") == count and d.get("hbm_bytes_per_launch"):
+            if (d.get("n_inputs") == n and d.get("count") == count and d.get("hbm_bytes_per_launch")
+                    and kernel and kernel in d.get("kernel", "")):
                 best = d
     return best
 
@@ -303,6 +310,7 @@ def main():
     ap.add_argument("--chunks", action="store_true")
     ap.add_argument("--roundtrip", action="store_true")
     ap.add_argument("--c2variants", action="store_true")
+    ap.add_argument("--crossover", action="store_true")
     args = ap.parse_args()
 
     dist = Dist(args.gpus)
@@ -314,6 +322,8 @@ def main():
         return chunks(args)
     if args.c2variants:
         return c2variants(args)
+    if args.crossover:
+        return crossover(args)
     if args.roundtrip:
         return roundtrip(args)
 
@@ -352,7 +362,7 @@ def main():
 
     parity = bool(dist.max(0.0 if parity in (True, None) else 1.0) == 0.0) if parity is not None else None
     copy_gbps = copy_ceiling() if dist.rank == 0 else None
-    prof = traffic_from_profiles(n, count)
+    prof = traffic_from_profiles(n, count) if cfg is None else None
     cpu = None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         cpu = cpu_baseline(n, count, args.cpu_budget)
@@ -464,6 +474,27 @@ def nway(args):
                           "frac_of_copy": round(b / t / 1e9 / copy_gbps, 4)}), flush=True)
       del ins, out
       torch.cuda.empty_cache()
+    return 0
+
+
+def crossover(args):
+    """Engine crossover: one-shot reduce of n = 2/4/8 inputs, 1-512 MiB per
+    input, f32 and bf16, TILE vs PHASE (sets the AUTO threshold)."""
+    for dtype in (torch.float32, torch.bfloat16):
+        esz = torch.tensor([], dtype=dtype).element_size()
+        for n in (2, 4, 8):
+            for mib in (1, 4, 16, 32, 64, 128, 256, 512):
+                count = (mib << 20) // esz
+                ins, out = make_bucket(n, count, dtype)
+                row = {"mode": "crossover", "dtype": str(dtype).split(".")[-1], "n": n, "mib_per_input": mib}
+                for eng, name in ((1, "tile"), (2, "phase"), (0, "auto")):
+                    _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins, config=dict(engine=eng)),
+                                          max(args.steps, 10), args.warmup)
+                    t = float(np.median(ms)) * 1e-3
+                    row[name + "_GBps"] = round((n + 1) * count * esz / t / 1e9, 1)
+                print(json.dumps(row), flush=True)
+                del ins, out
+                torch.cuda.empty_cache()
     return 0
 
 

@@ -640,7 +640,10 @@ constexpr int kDefPol = 11;  // nt loads, nt stores
 constexpr int kDefBpc = 1;
 constexpr int kPhBlock = 512;
 // auto engine: phased when the work gives every CU at least this many chunks
-constexpr uint64_t kPhaseMinChunksPerCU = 4;
+// and the computes sum at least kPhaseMinInputs inputs (on fewer streams the
+// tile order is as fast: profiles/r01_crossover.jsonl)
+constexpr uint64_t kPhaseMinChunksPerCU = 1;
+constexpr uint32_t kPhaseMinInputs = 5;
 
 // P of the phased engine: 16 packets per lane (acc + two in-flight loads =
 // 3 x 64 VGPRs at 512 lanes) unless the accumulator is wider than a packet
@@ -676,17 +679,19 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
   return r;
 }
 
-// Auto engine from the packets one input contributes (all computes of a launch).
-int auto_engine(uint64_t npkt, int dtype, int acc, int dev) {
+// Auto engine from the packets per input of a launch (summed over its
+// computes) and the number of inputs (packet-weighted mean for a plan).
+int auto_engine(uint64_t npkt, double n, int dtype, int acc, int dev) {
   const uint64_t chunk = (uint64_t)kPhBlock * phase_p_dtype(dtype, acc);
-  return npkt >= kPhaseMinChunksPerCU * (uint64_t)device_cus(dev) * chunk ? HICCL_ENGINE_PHASE
-                                                                           : HICCL_ENGINE_TILE;
+  return (n >= kPhaseMinInputs && npkt >= kPhaseMinChunksPerCU * (uint64_t)device_cus(dev) * chunk)
+             ? HICCL_ENGINE_PHASE
+             : HICCL_ENGINE_TILE;
 }
 
 // Fill in the engine and its default shape.
-void finish_cfg(Cfg &c, uint64_t npkt, int dtype, int dev) {
+void finish_cfg(Cfg &c, uint64_t npkt, int n, int dtype, int dev) {
   if (c.engine == HICCL_ENGINE_AUTO)
-    c.engine = (c.block || c.unroll) ? HICCL_ENGINE_TILE : auto_engine(npkt, dtype, c.acc, dev);
+    c.engine = (c.block || c.unroll) ? HICCL_ENGINE_TILE : auto_engine(npkt, n, dtype, c.acc, dev);
   if (c.engine == HICCL_ENGINE_PHASE) {
     if (!c.block) c.block = kPhBlock;
     if (!c.unroll) c.unroll = phase_p_dtype(dtype, c.acc);
@@ -867,7 +872,7 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
   hipStream_t s = (hipStream_t)stream;
   const int dev = current_device();
   Split sp = split_on(out, count, esz);
-  finish_cfg(c, sp.npkt, dtype, dev);
+  finish_cfg(c, sp.npkt, n, dtype, dev);
   if (n > kMaxArgInputs) return reduce_via_table(dtype, c.acc, c.engine, out, in, n, count, s);
 
   single_fn fn = pick_single_dtype(dtype, c);
@@ -959,9 +964,16 @@ int plan_upload(hiccl_reduce_plan *p) {
     return e;
   p->host_desc.assign(nc + 1, PlanDesc{});
   uint64_t total_pkt = 0;
-  for (auto &c : p->comps) total_pkt += split_on(c.out, c.count, p->esz).npkt;
-  p->engine = p->engine_req != HICCL_ENGINE_AUTO ? p->engine_req
-                                                 : auto_engine(total_pkt, p->dtype, p->acc, p->device);
+  double weighted_n = 0;
+  for (auto &c : p->comps) {
+    const uint64_t k = split_on(c.out, c.count, p->esz).npkt;
+    total_pkt += k;
+    weighted_n += (double)k * c.in.size();
+  }
+  const double mean_n = total_pkt ? weighted_n / total_pkt : 0;
+  p->engine = p->engine_req != HICCL_ENGINE_AUTO
+                  ? p->engine_req
+                  : auto_engine(total_pkt, mean_n, p->dtype, p->acc, p->device);
   const uint64_t unit = unit_pkts(p->engine, p->dtype, p->acc);
   uint64_t tile = 0;
   size_t off = 0;

@@ -56,7 +56,9 @@ typedef enum {
  *          ... (next input's loads in flight while the current one is
  *          added), then writes the chunk: only ~2 input streams are open
  *          chip-wide at a time.  Default for large buckets.
- *   AUTO   PHASE when every CU gets >= 4 chunks, else TILE. */
+ *   AUTO   PHASE when there are >= 5 inputs and every CU gets >= 1 chunk
+ *          (one-shot: that call; plan: all computes, packet-weighted mean
+ *          n), else TILE. */
 typedef enum {
   HICCL_ENGINE_AUTO = 0,
   HICCL_ENGINE_TILE = 1,

@@ -283,15 +283,17 @@ def test_plan_phase_engine(oracle, each):
 
 
 def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
-    """AUTO resolves to PHASE once every CU gets >= 4 chunks of 128 KiB
-    (f32: 2^25 elements per input on 256 CUs), to TILE below."""
-    count = 1 << 25
+    """AUTO resolves to PHASE with >= 5 inputs once every CU gets a chunk
+    of 128 KiB (f32: 2^23 elements per input on 256 CUs), to TILE below or
+    with fewer inputs."""
+    count = 1 << 23
     a = torch.empty(count, device=DEV)
     hiccl_amd.fill_uniform(a, 77, 0)
     out = torch.empty(count, device=DEV)
-    for cnt, expect in ((count, hiccl_amd.HICCL_ENGINE_PHASE), (1 << 20, hiccl_amd.HICCL_ENGINE_TILE)):
+    P, T = hiccl_amd.HICCL_ENGINE_PHASE, hiccl_amd.HICCL_ENGINE_TILE
+    for cnt, n, expect in ((count, 6, P), (count, 2, T), (count // 4, 6, T)):
         comp = hiccl_amd.Compute(torch.float32, device=0)
-        comp.add([a, a], out, cnt, compid=0)
+        comp.add([a] * n, out, cnt, compid=0)
         comp.start()
         comp.wait()
         if torch.cuda.get_device_properties(0).multi_processor_count == 256:
@@ -299,7 +301,10 @@ def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
         idx = np.array([0, 1, cnt // 2, cnt - 1], np.int64)
         exp = oracle.sample_sum(idx.astype(np.uint64), 77, 1)
         got = out[torch.from_numpy(idx).to(DEV)].cpu().numpy()
-        assert bits_equal(got, (exp + exp).astype(np.float32))
+        ref = np.zeros_like(exp)
+        for _ in range(n):
+            ref = (ref + exp).astype(np.float32)
+        assert bits_equal(got, ref)
         comp.close()
 
 

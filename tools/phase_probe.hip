@@ -128,6 +128,186 @@ __global__ __launch_bounds__(B) void k_phase_n(PArgs a) {
   }
 }
 
+// Phased, N static (8), D = 2, with order/store variants:
+//   MODE & 1: no store (read-only ceiling of the phased order)
+//   MODE & 2: slab order (workgroup b owns chunks [b*per, (b+1)*per))
+template <int B, int P, int MODE>
+__global__ __launch_bounds__(B) void k_phase_x(PArgs a) {
+  constexpr int N = 8;
+  constexpr uint64_t CH = (uint64_t)B * P * 16;
+  const uint64_t nch = (a.bytes + CH - 1) / CH;
+  uint32_t voff[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) voff[p] = (uint32_t)((p * B + threadIdx.x) * 16);
+  uint64_t c0 = blockIdx.x, c1 = nch, cs = gridDim.x;
+  if (MODE & 2) {
+    const uint64_t per = (nch + gridDim.x - 1) / gridDim.x;
+    c0 = blockIdx.x * per;
+    c1 = c0 + per < nch ? c0 + per : nch;
+    cs = 1;
+  }
+  f32x4 sink = (f32x4)(0.0f);
+  for (uint64_t c = c0; c < c1; c += cs) {
+    const uint64_t off = c * CH;
+    const uint32_t nb = (uint32_t)((a.bytes - off) < CH ? (a.bytes - off) : CH);
+    f32x4 acc[P], x[2][P];
+#pragma unroll
+    for (int p = 0; p < P; p++) acc[p] = (f32x4)(0.0f);
+    {
+      rsrc_t r = mk(a.in[0] + off, nb);
+#pragma unroll
+      for (int p = 0; p < P; p++) x[0][p] = ld<2>(r, voff[p]);
+    }
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      if (j + 1 < N) {
+        rsrc_t r = mk(a.in[j + 1] + off, nb);
+#pragma unroll
+        for (int p = 0; p < P; p++) x[(j + 1) & 1][p] = ld<2>(r, voff[p]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] += x[j & 1][p];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (MODE & 1) {
+#pragma unroll
+      for (int p = 0; p < P; p++) sink += acc[p];
+    } else {
+      rsrc_t w = mk(a.out + off, nb);
+#pragma unroll
+      for (int p = 0; p < P; p++)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[p]), w, (int)voff[p], 0, 2);
+    }
+  }
+  if ((MODE & 1) && sink.x == 1.2345f && sink.y == 5.4321f) a.out[threadIdx.x] = 1;
+}
+
+// Phased with a 2-part chunk: part 0's accumulator in registers, part 1's in
+// LDS (B*P*16 B); chunk = 2*B*P*16 B (256 KiB at 512 x 16).  Loads stream
+// (j,0), (j,1), (j+1,0), ...: one part in flight while the other is added.
+template <int B, int P>
+__global__ __launch_bounds__(B) void k_phase_lds(PArgs a) {
+  constexpr uint64_t PART = (uint64_t)B * P * 16;
+  constexpr uint64_t CH = 2 * PART;
+  __shared__ f32x4 lacc[P * B];
+  const uint64_t nch = (a.bytes + CH - 1) / CH;
+  uint32_t voff[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) voff[p] = (uint32_t)((p * B + threadIdx.x) * 16);
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    const uint64_t off0 = c * CH, off1 = off0 + PART;
+    const uint64_t left0 = a.bytes - off0;
+    const uint32_t nb0 = (uint32_t)(left0 < PART ? left0 : PART);
+    const uint32_t nb1 = (uint32_t)(left0 <= PART ? 0 : (left0 - PART < PART ? left0 - PART : PART));
+    f32x4 acc[P], x[P], y[P];
+#pragma unroll
+    for (int p = 0; p < P; p++) acc[p] = (f32x4)(0.0f);
+    {
+      rsrc_t r0 = mk(a.in[0] + off0, nb0);
+#pragma unroll
+      for (int p = 0; p < P; p++) x[p] = ld<2>(r0, voff[p]);
+      rsrc_t r1 = mk(a.in[0] + off1, nb1);
+#pragma unroll
+      for (int p = 0; p < P; p++) y[p] = ld<2>(r1, voff[p]);
+    }
+    for (int j = 0; j < a.n; j++) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] += x[p];
+      __builtin_amdgcn_sched_barrier(0);
+      const bool more = j + 1 < a.n;
+      {
+        rsrc_t r0 = mk(a.in[more ? j + 1 : j] + off0, more ? nb0 : 0u);
+#pragma unroll
+        for (int p = 0; p < P; p++) x[p] = ld<2>(r0, voff[p]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (j == 0) {
+#pragma unroll
+        for (int p = 0; p < P; p++) lacc[p * B + threadIdx.x] = (f32x4)(0.0f) + y[p];
+      } else {
+#pragma unroll
+        for (int p = 0; p < P; p++) lacc[p * B + threadIdx.x] += y[p];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        rsrc_t r1 = mk(a.in[more ? j + 1 : j] + off1, more ? nb1 : 0u);
+#pragma unroll
+        for (int p = 0; p < P; p++) y[p] = ld<2>(r1, voff[p]);
+      }
+    }
+    rsrc_t w0 = mk(a.out + off0, nb0), w1 = mk(a.out + off1, nb1);
+#pragma unroll
+    for (int p = 0; p < P; p++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[p]), w0, (int)voff[p], 0, 2);
+#pragma unroll
+    for (int p = 0; p < P; p++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lacc[p * B + threadIdx.x]), w1,
+                                             (int)voff[p], 0, 2);
+  }
+}
+
+// Phased, pipelined ACROSS chunks: the workgroup walks a flat sequence of
+// units (chunk c, input j) with two register buffers; the load of unit k+2
+// is issued right after unit k is added, so the next chunk's input 0 is in
+// flight while the current chunk's last input is added and stored.
+template <int B, int P>
+__global__ __launch_bounds__(B) void k_phase_flat(PArgs a) {
+  constexpr uint64_t CH = (uint64_t)B * P * 16;
+  const uint64_t nch = (a.bytes + CH - 1) / CH;
+  if (blockIdx.x >= nch) return;
+  const int n = a.n;
+  uint32_t voff[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) voff[p] = (uint32_t)((p * B + threadIdx.x) * 16);
+  // load cursor (unit to be loaded next)
+  uint64_t lc = blockIdx.x;
+  int lj = 0;
+  auto chunk_bytes = [&](uint64_t c) -> uint32_t {
+    const uint64_t left = a.bytes - c * CH;
+    return (uint32_t)(left < CH ? left : CH);
+  };
+  auto issue = [&](f32x4 (&buf)[P]) {
+    const bool valid = lc < nch;
+    rsrc_t r = mk(a.in[valid ? lj : 0] + (valid ? lc * CH : 0), valid ? chunk_bytes(lc) : 0u);
+#pragma unroll
+    for (int p = 0; p < P; p++) buf[p] = ld<2>(r, voff[p]);
+    if (++lj == n) { lj = 0; lc += gridDim.x; }
+  };
+  // add cursor
+  uint64_t ac = blockIdx.x;
+  int aj = 0;
+  f32x4 acc[P], x[P], y[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) acc[p] = (f32x4)(0.0f);
+  auto consume = [&](f32x4 (&buf)[P]) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int p = 0; p < P; p++) acc[p] += buf[p];
+    if (++aj == n) {
+      rsrc_t w = mk(a.out + ac * CH, chunk_bytes(ac));
+#pragma unroll
+      for (int p = 0; p < P; p++) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[p]), w, (int)voff[p], 0, 2);
+        acc[p] = (f32x4)(0.0f);
+      }
+      aj = 0;
+      ac += gridDim.x;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  issue(x);
+  issue(y);
+  while (ac < nch) {
+    consume(x);
+    issue(x);
+    if (ac >= nch) break;
+    consume(y);
+    issue(y);
+  }
+}
+
 // Product tile order (all n inputs of a tile loaded together), slab-walked.
 template <int B, int U, int AUXL, int AUXS>
 __global__ __launch_bounds__(B) void k_slab(PArgs a) {
@@ -200,6 +380,21 @@ int pp_run(int kind, int block, int param, int depth, int nt, int grid, const vo
     PN(256, 8, 2) PN(256, 16, 2) PN(512, 8, 2) PN(1024, 4, 2) PN(1024, 8, 2)
     PN(512, 8, 3) PN(1024, 4, 3) PN(512, 4, 3) PN(512, 4, 4) PN(1024, 8, 3) PN(256, 16, 3)
     PN(512, 16, 2)
+  } else if (kind == 3) {
+    if (block == 512 && param == 16) return launch(k_phase_lds<512, 16>, grid, 512, a, s);
+    if (block == 512 && param == 8) return launch(k_phase_lds<512, 8>, grid, 512, a, s);
+    if (block == 1024 && param == 8) return launch(k_phase_lds<1024, 8>, grid, 1024, a, s);
+    if (block == 256 && param == 16) return launch(k_phase_lds<256, 16>, grid, 256, a, s);
+  } else if (kind == 5) {
+    if (block == 512 && param == 16) return launch(k_phase_flat<512, 16>, grid, 512, a, s);
+    if (block == 512 && param == 8) return launch(k_phase_flat<512, 8>, grid, 512, a, s);
+    if (block == 1024 && param == 8) return launch(k_phase_flat<1024, 8>, grid, 1024, a, s);
+  } else if (kind == 4) {  // depth = MODE
+    if (n != 8) return -3;
+    if (block == 512 && param == 16 && depth == 0) return launch(k_phase_x<512, 16, 0>, grid, 512, a, s);
+    if (block == 512 && param == 16 && depth == 1) return launch(k_phase_x<512, 16, 1>, grid, 512, a, s);
+    if (block == 512 && param == 16 && depth == 2) return launch(k_phase_x<512, 16, 2>, grid, 512, a, s);
+    if (block == 512 && param == 16 && depth == 3) return launch(k_phase_x<512, 16, 3>, grid, 512, a, s);
   } else {
     SL(256, 4) SL(256, 2) SL(512, 4)
   }
