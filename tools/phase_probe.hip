@@ -131,7 +131,9 @@ __global__ __launch_bounds__(B) void k_phase_n(PArgs a) {
 // Phased, N static (8), D = 2, with order/store variants:
 //   MODE & 1: no store (read-only ceiling of the phased order)
 //   MODE & 2: slab order (workgroup b owns chunks [b*per, (b+1)*per))
-template <int B, int P, int MODE>
+//   MODE & 4: staggered start (workgroup b sleeps (b % 9) x ~5 us first)
+// AUXS: store cache-policy bits (gfx950: 1 sc0, 2 nt, 16 sc1).
+template <int B, int P, int MODE, int AUXS = 2>
 __global__ __launch_bounds__(B) void k_phase_x(PArgs a) {
   constexpr int N = 8;
   constexpr uint64_t CH = (uint64_t)B * P * 16;
@@ -147,6 +149,9 @@ __global__ __launch_bounds__(B) void k_phase_x(PArgs a) {
     cs = 1;
   }
   f32x4 sink = (f32x4)(0.0f);
+  if (MODE & 4) {
+    for (uint32_t k = 0; k < (blockIdx.x % 9) * 2; k++) __builtin_amdgcn_s_sleep(127);
+  }
   for (uint64_t c = c0; c < c1; c += cs) {
     const uint64_t off = c * CH;
     const uint32_t nb = (uint32_t)((a.bytes - off) < CH ? (a.bytes - off) : CH);
@@ -177,7 +182,7 @@ __global__ __launch_bounds__(B) void k_phase_x(PArgs a) {
       rsrc_t w = mk(a.out + off, nb);
 #pragma unroll
       for (int p = 0; p < P; p++)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[p]), w, (int)voff[p], 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[p]), w, (int)voff[p], 0, AUXS);
     }
   }
   if ((MODE & 1) && sink.x == 1.2345f && sink.y == 5.4321f) a.out[threadIdx.x] = 1;
@@ -308,6 +313,169 @@ __global__ __launch_bounds__(B) void k_phase_flat(PArgs a) {
   }
 }
 
+// Phased, pipelined across chunks with static buffer roles.  pass<A,B>:
+// A holds (chunk c, input 0) in flight on entry; on exit the buffer named by
+// the return value holds (next chunk, input 0): B for odd n, A for even n.
+// Odd n therefore runs chunk pairs (x,y) then (y,x); even n runs (x,y).
+template <int P>
+__device__ __forceinline__ void pp_load(f32x4 (&buf)[P], const char *base, uint32_t nb,
+                                        const uint32_t (&voff)[P]) {
+  rsrc_t r = mk(base, nb);
+#pragma unroll
+  for (int p = 0; p < P; p++) buf[p] = ld<2>(r, voff[p]);
+}
+
+template <int P>
+__device__ __forceinline__ void pp_add(f32x4 (&acc)[P], const f32x4 (&buf)[P]) {
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int p = 0; p < P; p++) acc[p] += buf[p];
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int P, bool ODD>
+__device__ __forceinline__ void pp_pass(f32x4 (&A)[P], f32x4 (&B)[P], const PArgs &a, uint64_t off,
+                                        uint32_t nb, uint64_t offn, uint32_t nbn,
+                                        const uint32_t (&voff)[P]) {
+  f32x4 acc[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) acc[p] = (f32x4)(0.0f);
+  const int n = a.n;
+  int j = 0;
+  for (; j + 2 < n; j += 2) {
+    pp_load(B, a.in[j + 1] + off, nb, voff);
+    pp_add(acc, A);
+    pp_load(A, a.in[j + 2] + off, nb, voff);
+    pp_add(acc, B);
+  }
+  if constexpr (ODD) {
+    pp_load(B, a.in[0] + offn, nbn, voff);
+    pp_add(acc, A);
+  } else {
+    pp_load(B, a.in[n - 1] + off, nb, voff);
+    pp_add(acc, A);
+    pp_load(A, a.in[0] + offn, nbn, voff);
+    pp_add(acc, B);
+  }
+  rsrc_t w = mk(a.out + off, nb);
+#pragma unroll
+  for (int p = 0; p < P; p++)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[p]), w, (int)voff[p], 0, 2);
+}
+
+template <int B, int P>
+__global__ __launch_bounds__(B) void k_phase_pipe(PArgs a) {
+  constexpr uint64_t CH = (uint64_t)B * P * 16;
+  const uint64_t nch = (a.bytes + CH - 1) / CH;
+  uint32_t voff[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) voff[p] = (uint32_t)((p * B + threadIdx.x) * 16);
+  auto nbytes = [&](uint64_t c) -> uint32_t {
+    if (c >= nch) return 0u;
+    const uint64_t left = a.bytes - c * CH;
+    return (uint32_t)(left < CH ? left : CH);
+  };
+  auto offs = [&](uint64_t c) -> uint64_t { return c < nch ? c * CH : 0; };
+  f32x4 x[P], y[P];
+  uint64_t c = blockIdx.x;
+  if (c >= nch) return;
+  pp_load(x, a.in[0] + offs(c), nbytes(c), voff);
+  const uint64_t g = gridDim.x;
+  if (a.n & 1) {
+    while (true) {
+      pp_pass<P, true>(x, y, a, offs(c), nbytes(c), offs(c + g), nbytes(c + g), voff);
+      c += g;
+      if (c >= nch) break;
+      pp_pass<P, true>(y, x, a, offs(c), nbytes(c), offs(c + g), nbytes(c + g), voff);
+      c += g;
+      if (c >= nch) break;
+    }
+  } else {
+    for (; c < nch; c += g) pp_pass<P, false>(x, y, a, offs(c), nbytes(c), offs(c + g), nbytes(c + g), voff);
+  }
+}
+
+// Phased (N = 8), with a soft grid barrier before each round's stores so the
+// output writes of all workgroups land together (one write burst per round
+// instead of a steady 1-in-9 write trickle).  Bounded spin (SPIN_TICKS of the
+// 100 MHz s_memrealtime clock): never hangs even if the grid is not fully
+// co-resident.  SYNC_EVERY: barrier every k rounds.
+__device__ unsigned int g_round_counter[64];
+
+template <int B, int P, int SYNC_EVERY>
+__global__ __launch_bounds__(B) void k_phase_sync(PArgs a, unsigned int *counter) {
+  constexpr int N = 8;
+  constexpr uint64_t CH = (uint64_t)B * P * 16;
+  constexpr uint64_t SPIN_TICKS = 20000;  // 200 us
+  const uint64_t nch = (a.bytes + CH - 1) / CH;
+  uint32_t voff[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) voff[p] = (uint32_t)((p * B + threadIdx.x) * 16);
+  __shared__ int go;
+  unsigned int round = 0;
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x, round++) {
+    const uint64_t off = c * CH;
+    const uint32_t nb = (uint32_t)((a.bytes - off) < CH ? (a.bytes - off) : CH);
+    f32x4 acc[P], x[2][P];
+#pragma unroll
+    for (int p = 0; p < P; p++) acc[p] = (f32x4)(0.0f);
+    {
+      rsrc_t r = mk(a.in[0] + off, nb);
+#pragma unroll
+      for (int p = 0; p < P; p++) x[0][p] = ld<2>(r, voff[p]);
+    }
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      if (j + 1 < N) {
+        rsrc_t r = mk(a.in[j + 1] + off, nb);
+#pragma unroll
+        for (int p = 0; p < P; p++) x[(j + 1) & 1][p] = ld<2>(r, voff[p]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] += x[j & 1][p];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (round % SYNC_EVERY == 0) {
+      if (threadIdx.x == 0) {
+        // workgroups that own a chunk in this round
+        const uint64_t first = (uint64_t)round * gridDim.x;
+        const uint64_t active = (nch - first) < gridDim.x ? (nch - first) : gridDim.x;
+        const unsigned int target = (unsigned int)(first + active);
+        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          __builtin_amdgcn_s_sleep(8);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS) break;
+        }
+        go = 1;
+      }
+      __syncthreads();
+    } else {
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    rsrc_t w = mk(a.out + off, nb);
+#pragma unroll
+    for (int p = 0; p < P; p++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[p]), w, (int)voff[p], 0, 2);
+  }
+  (void)go;
+}
+
+static unsigned int *sync_counter() {
+  static unsigned int *p = nullptr;
+  if (!p) (void)hipGetSymbolAddress((void **)&p, HIP_SYMBOL(g_round_counter));
+  return p;
+}
+
+template <int SE>
+static int launch_sync(int grid, const PArgs &a, hipStream_t s) {
+  unsigned int *ctr = sync_counter();
+  if (hipMemsetAsync(ctr, 0, 64 * sizeof(unsigned int), s)) return -5;
+  hipLaunchKernelGGL((k_phase_sync<512, 16, SE>), dim3(grid), dim3(512), 0, s, a, ctr);
+  return (int)hipGetLastError();
+}
+
 // Product tile order (all n inputs of a tile loaded together), slab-walked.
 template <int B, int U, int AUXL, int AUXS>
 __global__ __launch_bounds__(B) void k_slab(PArgs a) {
@@ -389,12 +557,30 @@ int pp_run(int kind, int block, int param, int depth, int nt, int grid, const vo
     if (block == 512 && param == 16) return launch(k_phase_flat<512, 16>, grid, 512, a, s);
     if (block == 512 && param == 8) return launch(k_phase_flat<512, 8>, grid, 512, a, s);
     if (block == 1024 && param == 8) return launch(k_phase_flat<1024, 8>, grid, 1024, a, s);
+  } else if (kind == 6) {
+    if (block == 512 && param == 16) return launch(k_phase_pipe<512, 16>, grid, 512, a, s);
+    if (block == 512 && param == 8) return launch(k_phase_pipe<512, 8>, grid, 512, a, s);
+    if (block == 1024 && param == 8) return launch(k_phase_pipe<1024, 8>, grid, 1024, a, s);
+  } else if (kind == 7) {  // depth = SYNC_EVERY
+    if (n != 8 || block != 512 || param != 16) return -3;
+    if (depth == 1) return launch_sync<1>(grid, a, s);
+    if (depth == 2) return launch_sync<2>(grid, a, s);
+    if (depth == 4) return launch_sync<4>(grid, a, s);
   } else if (kind == 4) {  // depth = MODE
     if (n != 8) return -3;
     if (block == 512 && param == 16 && depth == 0) return launch(k_phase_x<512, 16, 0>, grid, 512, a, s);
     if (block == 512 && param == 16 && depth == 1) return launch(k_phase_x<512, 16, 1>, grid, 512, a, s);
     if (block == 512 && param == 16 && depth == 2) return launch(k_phase_x<512, 16, 2>, grid, 512, a, s);
     if (block == 512 && param == 16 && depth == 3) return launch(k_phase_x<512, 16, 3>, grid, 512, a, s);
+    if (block == 512 && param == 16 && depth == 4) return launch(k_phase_x<512, 16, 4>, grid, 512, a, s);
+    if (block == 512 && param == 16 && depth == 5) return launch(k_phase_x<512, 16, 5>, grid, 512, a, s);
+    // depth 16+: store policy variants (aux = depth - 16)
+    if (block == 512 && param == 16 && depth == 16 + 3) return launch(k_phase_x<512, 16, 0, 3>, grid, 512, a, s);
+    if (block == 512 && param == 16 && depth == 16 + 16) return launch(k_phase_x<512, 16, 0, 16>, grid, 512, a, s);
+    if (block == 512 && param == 16 && depth == 16 + 17) return launch(k_phase_x<512, 16, 0, 17>, grid, 512, a, s);
+    if (block == 512 && param == 16 && depth == 16 + 18) return launch(k_phase_x<512, 16, 0, 18>, grid, 512, a, s);
+    if (block == 512 && param == 16 && depth == 16 + 19) return launch(k_phase_x<512, 16, 0, 19>, grid, 512, a, s);
+    if (block == 512 && param == 16 && depth == 16 + 1) return launch(k_phase_x<512, 16, 0, 1>, grid, 512, a, s);
   } else {
     SL(256, 4) SL(256, 2) SL(512, 4)
   }

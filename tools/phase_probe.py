@@ -27,6 +27,12 @@ P.pp_diff.restype = ctypes.c_longlong
 P.pp_diff.argtypes = [vp, vp, ctypes.c_uint64]
 P.pp_granularity.restype = ctypes.c_uint64
 
+H = None
+if os.path.exists(os.path.join(ROOT, "tools", "libhbm_probe.so")):
+    H = ctypes.CDLL(os.path.join(ROOT, "tools", "libhbm_probe.so"))
+    H.probe_run.restype = ctypes.c_int
+    H.probe_run.argtypes = [ctypes.c_int] * 7 + [vp, ctypes.c_int, vp, ctypes.c_uint64, vp]
+
 N, COUNT = 8, 1 << 28
 NB = COUNT * 4
 
@@ -59,10 +65,8 @@ def main():
     modes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2").split(",")]
     buckets = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     # (kind, block, param, depth, nt, grid); kind 0 phase (runtime n), 1 slab, 2 phase_n (n = 8)
-    variants = [(2, 512, 16, 2, 1, 256), (4, 512, 16, 0, 1, 256), (4, 512, 16, 1, 1, 256),
-                (4, 512, 16, 2, 1, 256), (4, 512, 16, 3, 1, 256), (3, 512, 16, 0, 1, 256),
-                (3, 1024, 8, 0, 1, 256), (3, 512, 8, 0, 1, 256), (5, 512, 16, 0, 1, 256),
-                (5, 512, 8, 0, 1, 256), (5, 512, 8, 0, 1, 512)]
+    variants = [(4, 512, 16, 0, 1, 256), (7, 512, 16, 1, 1, 256), (7, 512, 16, 2, 1, 256),
+                (7, 512, 16, 4, 1, 256), (4, 512, 16, 0, 1, 256), (7, 512, 16, 1, 1, 256)]
     g = P.pp_granularity()
     print(json.dumps({"vmm_granularity_min": g >> 32, "vmm_granularity_rec": g & 0xffffffff}), flush=True)
     stream = torch.cuda.current_stream()
@@ -93,11 +97,21 @@ def main():
                     continue
                 ms = timeit(fn)
                 torch.cuda.synchronize()
-                diff = P.pp_diff(vp(out), vp(ref), NB) if not (kind == 4 and depth & 1) else None
+                diff = P.pp_diff(vp(out), vp(ref), NB) if not (kind == 4 and depth < 16 and depth & 1) else None
                 print(json.dumps({"alloc": mode, "bucket": b,
-                                  "kernel": ["phase", "slab", "phase_n", "phase_lds", "phase_x", "phase_flat"][kind], "block": block,
+                                  "kernel": ["phase", "slab", "phase_n", "phase_lds", "phase_x", "phase_flat", "phase_pipe", "phase_sync"][kind], "block": block,
                                   "param": param, "depth": depth, "nt": nt, "grid": grid, "ms": round(ms, 4),
                                   "GBps": round(9 * NB / ms / 1e6, 1), "mismatch_words": diff}), flush=True)
+            if H is not None:
+                for g in (256, 1024):
+                    fn = lambda: H.probe_run(2, 256, 4, 2, 2, 0, g, tab, N, vp(out), NB, sh)
+                    ms = timeit(fn)
+                    print(json.dumps({"alloc": mode, "bucket": b, "kernel": "write_only(hbm_probe)", "grid": g,
+                                      "ms": round(ms, 4), "GBps": round(NB / ms / 1e6, 1)}), flush=True)
+                fn = lambda: H.probe_run(1, 256, 4, 2, 2, 0, 256, tab, N, vp(out), NB, sh)
+                ms = timeit(fn)
+                print(json.dumps({"alloc": mode, "bucket": b, "kernel": "read_only_tile(hbm_probe)",
+                                  "ms": round(ms, 4), "GBps": round(N * NB / ms / 1e6, 1)}), flush=True)
             ms = timeit(prod)
             print(json.dumps({"alloc": mode, "bucket": b, "kernel": "product(again)", "ms": round(ms, 4),
                               "GBps": round(9 * NB / ms / 1e6, 1)}), flush=True)
