@@ -115,6 +115,7 @@ __device__ __forceinline__ uint16_t bf_round(float f) {
 // reference's `T acc = 0; acc += x` (so -0 inputs sum to +0).
 
 struct OpF32 {
+  static constexpr bool kWidens = false;
   static constexpr int kEsz = 4;
   typedef f32x4 acc_t;
   __device__ static acc_t zero() { return (f32x4)(0.0f); }
@@ -127,6 +128,7 @@ struct OpF32 {
 };
 
 struct OpF64 {
+  static constexpr bool kWidens = false;
   static constexpr int kEsz = 8;
   typedef f64x2 acc_t;
   __device__ static acc_t zero() { return (f64x2)(0.0); }
@@ -139,6 +141,7 @@ struct OpF64 {
 };
 
 struct OpU64 {
+  static constexpr bool kWidens = false;
   static constexpr int kEsz = 8;
   typedef u64x2 acc_t;
   __device__ static acc_t zero() { return (u64x2)(0); }
@@ -151,6 +154,7 @@ struct OpU64 {
 };
 
 struct OpI32 {  // two's-complement wrap-around, done in unsigned
+  static constexpr bool kWidens = false;
   static constexpr int kEsz = 4;
   typedef u32x4 acc_t;
   __device__ static acc_t zero() { return (u32x4)(0u); }
@@ -163,29 +167,32 @@ struct OpI32 {  // two's-complement wrap-around, done in unsigned
 };
 
 // bf16, reference semantics: acc is bf16, every add = f32 add then round to
-// bf16.  The accumulator is kept as f32 values that are exact bf16 numbers.
+// bf16.  The accumulator is kept PACKED (8 bf16 in a u32x4, the packet's own
+// layout): widen both operands (exact), add in f32, round-to-nearest-even
+// back (v_cvt_pk_bf16_f32).  4 VGPRs per packet, so the phased engine runs
+// bf16 at the same 128 KiB chunk as f32.
+// The pack is an opaque v_cvt_pk_bf16_f32 (the same instruction the __bf16
+// casts lower to) so the compiler cannot see through pack->widen and keep the
+// accumulator widened in 8 VGPRs per packet (it does, and spills).
+__device__ __forceinline__ uint32_t bf_pack_opaque(float lo, float hi) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+
 struct OpBF16 {
+  static constexpr bool kWidens = true;
   static constexpr int kEsz = 2;
-  typedef f32x8 acc_t;
-  __device__ static acc_t zero() { return (f32x8)(0.0f); }
+  typedef u32x4 acc_t;
+  __device__ static acc_t zero() { return (u32x4)(0u); }  // +0 bf16
   __device__ static acc_t add(acc_t a, u32x4 p) {
     acc_t r;
 #pragma unroll
-    for (int w = 0; w < 4; w++) {
-      float s0 = a[2 * w] + bf_lo(p[w]);
-      float s1 = a[2 * w + 1] + bf_hi(p[w]);
-      uint32_t q = bf_pack(s0, s1);
-      r[2 * w] = bf_lo(q);
-      r[2 * w + 1] = bf_hi(q);
-    }
+    for (int w = 0; w < 4; w++)
+      r[w] = bf_pack_opaque(bf_lo(a[w]) + bf_lo(p[w]), bf_hi(a[w]) + bf_hi(p[w]));
     return r;
   }
-  __device__ static u32x4 pack(acc_t a) {
-    u32x4 r;
-#pragma unroll
-    for (int w = 0; w < 4; w++) r[w] = bf_pack(a[2 * w], a[2 * w + 1]);
-    return r;
-  }
+  __device__ static u32x4 pack(acc_t a) { return a; }
   typedef float sacc_t;
   __device__ static sacc_t szero() { return 0.0f; }
   __device__ static sacc_t sadd(sacc_t a, const char *p) {
@@ -197,6 +204,7 @@ struct OpBF16 {
 
 // bf16 inputs, f32 accumulator, one rounding at the end (HICCL_ACC_WIDE).
 struct OpBF16Wide {
+  static constexpr bool kWidens = true;
   static constexpr int kEsz = 2;
   typedef f32x8 acc_t;
   __device__ static acc_t zero() { return (f32x8)(0.0f); }
@@ -225,6 +233,7 @@ struct OpBF16Wide {
 // Exact byte copy (HICCL_BYTES): one input, out = in[0] bit for bit.  The
 // transport's batched data movement runs on the same tile engine.
 struct OpRaw {
+  static constexpr bool kWidens = false;
   static constexpr int kEsz = 1;
   typedef u32x4 acc_t;
   __device__ static acc_t zero() { return (u32x4)(0u); }
@@ -365,7 +374,10 @@ __device__ __forceinline__ void chunk_body(char *outb, Inputs in, uint32_t n, ui
       for (int p = 0; p < P; p++) y[p] = load_pkt<POL>(ry, voff[p]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int p = 0; p < P; p++) acc[p] = Op::add(acc[p], x[p]);
+      for (int p = 0; p < P; p++) {
+        acc[p] = Op::add(acc[p], x[p]);
+        if constexpr (Op::kWidens) __builtin_amdgcn_sched_barrier(0);
+      }
       __builtin_amdgcn_sched_barrier(0);
       const bool more = j + 2 < n;
       rsrc_t rx = make_rsrc(in(more ? j + 2 : j + 1) + off, more ? nbytes : 0u);
@@ -373,7 +385,10 @@ __device__ __forceinline__ void chunk_body(char *outb, Inputs in, uint32_t n, ui
       for (int p = 0; p < P; p++) x[p] = load_pkt<POL>(rx, voff[p]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int p = 0; p < P; p++) acc[p] = Op::add(acc[p], y[p]);
+      for (int p = 0; p < P; p++) {
+        acc[p] = Op::add(acc[p], y[p]);
+        if constexpr (Op::kWidens) __builtin_amdgcn_sched_barrier(0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if (n & 1) {
@@ -632,7 +647,8 @@ int check_buffers(void *out, const void *const *in, int n, size_t count, size_t 
 //  tile   256 lanes x 4 packets (16 KiB per input per tile), for computes too
 //         small to give every CU several phased chunks;
 //  phase  512 lanes x P packets (P = 16, or 8 where the accumulator of a
-//         packet takes 8 VGPRs: bf16) -- 128 KiB per input per chunk.
+//         packet takes 8 VGPRs -- bf16 WIDE -- or the adds get reassociated:
+//         int32) -- 128 KiB per input per chunk (64 KiB at P = 8).
 // Both: nt loads and nt stores, one workgroup per CU, grid-stride.
 constexpr int kDefBlock = 256;
 constexpr int kDefUnroll = 4;
@@ -655,8 +671,8 @@ constexpr int phase_p() {
 }
 
 int phase_p_dtype(int dtype, int acc) {
-  (void)acc;
-  return (dtype == HICCL_BFLOAT16 || dtype == HICCL_INT32) ? 8 : 16;
+  if (dtype == HICCL_BFLOAT16) return acc == HICCL_ACC_WIDE ? 8 : 16;
+  return dtype == HICCL_INT32 ? 8 : 16;
 }
 
 struct Cfg {

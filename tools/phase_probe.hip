@@ -476,6 +476,77 @@ static int launch_sync(int grid, const PArgs &a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Phased with split units: a chunk = Q units of B*U packets; the unit
+// sequence (j,0), (j,1), ..., (j,Q-1), (j+1,0), ... is double-buffered, so
+// the two units in flight are different inputs at offsets one unit apart
+// (not the same offset), and the in-flight buffers are U (not Q*U) packets
+// per lane: acc Q*U + 2*U packets.  Q even.
+template <int B, int U, int Q>
+__global__ __launch_bounds__(B) void k_phase_q(PArgs a) {
+  static_assert(Q % 2 == 0, "Q even");
+  constexpr uint64_t UB = (uint64_t)B * U * 16;
+  constexpr uint64_t CH = UB * Q;
+  const uint64_t nch = (a.bytes + CH - 1) / CH;
+  const int n = a.n;
+  uint32_t voff[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * B + threadIdx.x) * 16);
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    const uint64_t off = c * CH;
+    uint32_t nb[Q];
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const uint64_t o = off + q * UB;
+      nb[q] = o >= a.bytes ? 0u : (uint32_t)((a.bytes - o) < UB ? (a.bytes - o) : UB);
+    }
+    f32x4 acc[Q][U], x[U], y[U];
+#pragma unroll
+    for (int q = 0; q < Q; q++)
+#pragma unroll
+      for (int u = 0; u < U; u++) acc[q][u] = (f32x4)(0.0f);
+    {
+      rsrc_t r = mk(a.in[0] + off, nb[0]);
+#pragma unroll
+      for (int u = 0; u < U; u++) x[u] = ld<2>(r, voff[u]);
+    }
+    for (int j = 0; j < n; j++) {
+      const bool more = j + 1 < n;
+#pragma unroll
+      for (int q = 0; q < Q; q += 2) {
+        {  // y <- (j, q+1)
+          rsrc_t r = mk(a.in[j] + off + (q + 1) * UB, nb[q + 1]);
+#pragma unroll
+          for (int u = 0; u < U; u++) y[u] = ld<2>(r, voff[u]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; u++) acc[q][u] += x[u];
+        __builtin_amdgcn_sched_barrier(0);
+        {  // x <- (j, q+2) or (j+1, 0) or nothing
+          const bool last = q + 2 >= Q;
+          const int jj = last ? (more ? j + 1 : j) : j;
+          const uint64_t o = last ? off : off + (q + 2) * UB;
+          const uint32_t m = last ? (more ? nb[0] : 0u) : nb[(q + 2) % Q];
+          rsrc_t r = mk(a.in[jj] + o, m);
+#pragma unroll
+          for (int u = 0; u < U; u++) x[u] = ld<2>(r, voff[u]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; u++) acc[q + 1][u] += y[u];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      rsrc_t w = mk(a.out + off + q * UB, nb[q]);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[q][u]), w, (int)voff[u], 0, 2);
+    }
+  }
+}
+
 // Product tile order (all n inputs of a tile loaded together), slab-walked.
 template <int B, int U, int AUXL, int AUXS>
 __global__ __launch_bounds__(B) void k_slab(PArgs a) {
@@ -547,7 +618,8 @@ int pp_run(int kind, int block, int param, int depth, int nt, int grid, const vo
     if (n != 8) return -3;
     PN(256, 8, 2) PN(256, 16, 2) PN(512, 8, 2) PN(1024, 4, 2) PN(1024, 8, 2)
     PN(512, 8, 3) PN(1024, 4, 3) PN(512, 4, 3) PN(512, 4, 4) PN(1024, 8, 3) PN(256, 16, 3)
-    PN(512, 16, 2)
+    PN(512, 16, 2) PN(512, 12, 2) PN(512, 14, 2) PN(256, 24, 2) PN(256, 32, 2) PN(256, 36, 2)
+    PN(1024, 6, 2) PN(768, 8, 2)
   } else if (kind == 3) {
     if (block == 512 && param == 16) return launch(k_phase_lds<512, 16>, grid, 512, a, s);
     if (block == 512 && param == 8) return launch(k_phase_lds<512, 8>, grid, 512, a, s);
@@ -566,6 +638,15 @@ int pp_run(int kind, int block, int param, int depth, int nt, int grid, const vo
     if (depth == 1) return launch_sync<1>(grid, a, s);
     if (depth == 2) return launch_sync<2>(grid, a, s);
     if (depth == 4) return launch_sync<4>(grid, a, s);
+  } else if (kind == 8) {  // param = U, depth = Q
+    if (block == 512 && param == 8 && depth == 2) return launch(k_phase_q<512, 8, 2>, grid, 512, a, s);
+    if (block == 512 && param == 4 && depth == 4) return launch(k_phase_q<512, 4, 4>, grid, 512, a, s);
+    if (block == 512 && param == 8 && depth == 4) return launch(k_phase_q<512, 8, 4>, grid, 512, a, s);
+    if (block == 512 && param == 4 && depth == 8) return launch(k_phase_q<512, 4, 8>, grid, 512, a, s);
+    if (block == 1024 && param == 4 && depth == 2) return launch(k_phase_q<1024, 4, 2>, grid, 1024, a, s);
+    if (block == 1024 && param == 4 && depth == 4) return launch(k_phase_q<1024, 4, 4>, grid, 1024, a, s);
+    if (block == 256 && param == 8 && depth == 8) return launch(k_phase_q<256, 8, 8>, grid, 256, a, s);
+    if (block == 512 && param == 6 && depth == 4) return launch(k_phase_q<512, 6, 4>, grid, 512, a, s);
   } else if (kind == 4) {  // depth = MODE
     if (n != 8) return -3;
     if (block == 512 && param == 16 && depth == 0) return launch(k_phase_x<512, 16, 0>, grid, 512, a, s);
