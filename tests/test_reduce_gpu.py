@@ -352,6 +352,27 @@ def test_full_size_sampled(oracle, count, eng):
     assert bits_equal(got2, oracle.sample_sum(idx2.astype(np.uint64), seed, n))
 
 
+@pytest.mark.parametrize("n,log2count", [(2, 24), (5, 24), (16, 23), (64, 22)])
+@pytest.mark.parametrize("eng", [None, PHASE, dict(engine=hiccl_amd.HICCL_ENGINE_TILE)],
+                         ids=["auto", "phase", "tile"])
+def test_nway_sampled(oracle, n, log2count, eng):
+    """Config-3 shapes (N-way sweep) at 16-64 MiB per input: 4096 sampled
+    indices + both ends against the oracle generator, every engine."""
+    count, seed = (1 << log2count) + 7, 99
+    ins = [torch.empty(count, device=DEV) for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, seed, k)
+    out = torch.empty(count, device=DEV)
+    hiccl_amd.reduce(out, ins, config=eng)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(n)
+    idx = np.concatenate([np.arange(40), count - 40 + np.arange(40),
+                          rng.integers(0, count, 4096)]).astype(np.int64)
+    got = out[torch.from_numpy(idx).to(DEV)].cpu().numpy()
+    exp = oracle.sample_sum(idx.astype(np.uint64), seed, n)
+    assert bits_equal(got, exp), first_mismatch(got, exp)
+
+
 @pytest.mark.parametrize("dtype", [np.float32, np.uint16])
 @pytest.mark.parametrize("engine", [hiccl_amd.HICCL_ENGINE_AUTO, hiccl_amd.HICCL_ENGINE_PHASE])
 def test_plan_partitioned_on_default_stream(oracle, dtype, engine):
