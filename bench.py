@@ -12,7 +12,10 @@ Extra objects on the JSON line:
   roofline      achieved = algorithmic bytes per launch / mean kernel time from
                 HIP events on the launch stream; peak = 8000 GB/s (MI355X HBM3E
                 spec); traffic = PMC HBM bytes per launch from the committed
-                profiles/ PMC summary when one matches this workload, else null.
+                profiles/ PMC summary when one matches this workload AND
+                kernel, else null; plus measured ceilings on the same
+                buckets: 8R+1W XOR probe, 8-stream read-only probe (tile
+                order), plain copy.
   cpu_baseline  the reference's own CPU reduce_kernel (compute.h:14-23, built
                 from /root/reference into oracle/_ref by oracle/build_ref.sh;
                 kind "reference") or the C restatement (kind "port"), timed on
@@ -140,10 +143,11 @@ def time_launches(fn, steps, warmup, dist=None):
     return t1 - t0, [a.elapsed_time(b) for a, b in evs]
 
 
-def mix_ceiling(ins, out, count, reps=10):
+def mix_ceiling(ins, out, count, reps=10, mode=0):
     """Achievable HBM rate for this very access mix (n streams read + 1
-    written, 16 B/lane, XOR instead of add) from tools/libhbm_probe.so, at
-    the reduction kernel's geometry and at grid 192; None if not built."""
+    written, 16 B/lane, XOR instead of add; mode 1: the n reads only) from
+    tools/libhbm_probe.so, tile order, at grids 256 and 192; None if not
+    built.  Rate = bytes the probe moves / time."""
     pso = os.path.join(ROOT, "tools", "libhbm_probe.so")
     if not os.path.exists(pso):
         return None
@@ -156,10 +160,11 @@ def mix_ceiling(ins, out, count, reps=10):
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     best = 0.0
     for grid in (256, 192):
-        fn = lambda: probe.probe_run(0, 256, 4, 2, 2, 0, grid, tab, n, ctypes.c_void_p(out.data_ptr()),  # noqa: E731
+        fn = lambda: probe.probe_run(mode, 256, 4, 2, 2, 0, grid, tab, n, ctypes.c_void_p(out.data_ptr()),  # noqa: E731
                                      count * 4, st)
         _, ms = time_launches(fn, reps, 3)
-        best = max(best, (n + 1) * count * 4 / (np.median(ms) * 1e-3) / 1e9)
+        moved = (n + (1 if mode == 0 else 0)) * count * 4
+        best = max(best, moved / (np.median(ms) * 1e-3) / 1e9)
     return best
 
 
@@ -357,6 +362,7 @@ def main():
         if not parity:
             log("bench: PARITY FAILURE against the oracle sample")
     mix_gbps = mix_ceiling(ins, out, count) if dist.rank == 0 else None
+    read_gbps = mix_ceiling(ins, out, count, mode=1) if dist.rank == 0 else None
     del ins, out
     torch.cuda.empty_cache()
 
@@ -393,6 +399,8 @@ def main():
                      "kernel_ms_mean": round(kern_s * 1e3, 4), "kernel_ms_min": round(min(kms), 4),
                      "mix_ceiling_GBps": round(mix_gbps, 1) if mix_gbps else None,
                      "frac_of_mix_ceiling": round(achieved / mix_gbps, 4) if mix_gbps else None,
+                     "read_ceiling_GBps": round(read_gbps, 1) if read_gbps else None,
+                     "frac_of_read_ceiling": round(achieved / read_gbps, 4) if read_gbps else None,
                      "copy_ceiling_GBps": round(copy_gbps, 1) if copy_gbps else None,
                      "frac_of_copy": round(achieved / copy_gbps, 4) if copy_gbps else None,
                      "traffic_source": (prof or {}).get("source")},
