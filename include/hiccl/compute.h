@@ -78,7 +78,16 @@ class Compute {
     numcomp++;
 #ifndef HICCL_PORT_HOST
     static_assert(dtype_of<T>() >= 0, "HiCCL::Compute: unsupported element type");
-    if (!plan) check(hiccl_reduce_plan_create(&plan, dtype_of<T>(), CommBench::mydevice), "plan_create");
+    if (!plan) {
+      check(hiccl_reduce_plan_create(&plan, dtype_of<T>(), CommBench::mydevice), "plan_create");
+      // HICCL_ENGINE=tile|phase|auto pins the kernel engine (same bits either
+      // way, so ranks need not agree); default auto.
+      if (const char *e = std::getenv("HICCL_ENGINE")) {
+        const std::string v(e);
+        const int eng = v == "tile" ? HICCL_ENGINE_TILE : v == "phase" ? HICCL_ENGINE_PHASE : HICCL_ENGINE_AUTO;
+        check(hiccl_reduce_plan_set_engine(plan, eng), "plan_set_engine");
+      }
+    }
     check(hiccl_reduce_plan_add(plan, out, (const void *const *)in.data(), (int)in.size(), n), "plan_add");
 #endif
   }

@@ -68,8 +68,14 @@ def test_invalid_arguments_rejected_on_host():
     # unsupported tuning config
     cfg = L.ReduceConfig(block=128)
     assert lib.hiccl_reduce_ex(0, ctypes.c_void_p(0x1000), _tab([0x2000]), 1, 4, None, ctypes.byref(cfg)) == 1
+    # unknown engine
+    cfg = L.ReduceConfig(engine=7)
+    assert lib.hiccl_reduce_ex(0, ctypes.c_void_p(0x1000), _tab([0x2000]), 1, 4, None, ctypes.byref(cfg)) == 1
+    assert "engine" in L.last_error()
     # plan NULL handling
     assert lib.hiccl_reduce_plan_launch(None, None) == 1
+    assert lib.hiccl_reduce_plan_set_engine(None, L.HICCL_ENGINE_PHASE) == 1
+    assert lib.hiccl_reduce_plan_engine(None) == -1
     assert lib.hiccl_reduce_plan_numcomp(None) == 0
     lib.hiccl_reduce_plan_destroy(None)
 

@@ -28,10 +28,10 @@ HIP = os.path.join(ROOT, "build", "collectives_hip")
 HIP_F32 = os.path.join(ROOT, "build", "collectives_hip_f32")
 
 
-def mpirun(np_, exe, args, timeout=180, streamed=True, fused=False):
+def mpirun(np_, exe, args, timeout=180, streamed=True, fused=False, engine="auto"):
     assert np_ <= 8
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED="1" if streamed else "0",
-               HICCL_FUSED_GATHER="1" if fused else "0", HICCL_SIGNAL_TIMEOUT="10")
+               HICCL_FUSED_GATHER="1" if fused else "0", HICCL_SIGNAL_TIMEOUT="10", HICCL_ENGINE=engine)
     cmd = ["timeout", "-k", "10", str(timeout), MPIRUN, "-np", str(np_), exe] + [str(a) for a in args]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd="/tmp")
     return p.returncode, p.stdout + p.stderr
@@ -66,13 +66,17 @@ def test_known_answer_fused_gather(np_, hier, libs, pattern, streamed):
     (8, 4099, 1, 1, 4, "1,4,2", "mpi,ipc,ipc"),
     (8, 4099, 1, 2, 2, "2,4", "ipc,ipc_get"),
 ])
-@pytest.mark.parametrize("streamed,fused", [(True, False), (False, False), (True, True), (False, True)],
-                         ids=["stream", "host", "stream-fused", "host-fused"])
+@pytest.mark.parametrize("streamed,fused,engine", [(True, False, "auto"), (False, False, "auto"),
+                                                   (True, True, "auto"), (False, True, "auto"),
+                                                   (False, False, "phase"), (True, True, "phase")],
+                         ids=["stream", "host", "stream-fused", "host-fused", "host-phase", "stream-fused-phase"])
 def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ring, depth, hier, libs, streamed,
-                                        fused):
+                                        fused, engine):
+    """HICCL_ENGINE=phase forces the input-phased engine on every step's
+    batched plan (these shapes would pick the tile engine)."""
     prefix = str(tmp_path / "ar")
     rc, out = mpirun(np_, HIP_F32, [8, count, stripe, ring, depth, 0, 0, hier, libs, prefix], streamed=streamed,
-                     fused=fused)
+                     fused=fused, engine=engine)
     assert rc == 0, out[-3000:]
     n = count * np_
     x = {r: oracle.fill(r + 1, n, 1234)[r] for r in range(np_)}
