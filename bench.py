@@ -316,6 +316,7 @@ def main():
     ap.add_argument("--roundtrip", action="store_true")
     ap.add_argument("--c2variants", action="store_true")
     ap.add_argument("--crossover", action="store_true")
+    ap.add_argument("--planvs", action="store_true")
     args = ap.parse_args()
 
     dist = Dist(args.gpus)
@@ -329,6 +330,8 @@ def main():
         return c2variants(args)
     if args.crossover:
         return crossover(args)
+    if args.planvs:
+        return planvs(args)
     if args.roundtrip:
         return roundtrip(args)
 
@@ -482,6 +485,42 @@ def nway(args):
                           "frac_of_copy": round(b / t / 1e9 / copy_gbps, 4)}), flush=True)
       del ins, out
       torch.cuda.empty_cache()
+    return 0
+
+
+def planvs(args):
+    """Plan-kernel overhead on the C2 bucket: one-shot launch vs a plan of
+    1, 1024 (1 MiB) and 8192 (128 KiB) computes, interleaved rounds."""
+    n, count = 8, 1 << 28
+    ins, out = make_bucket(n, count)
+    stream = torch.cuda.current_stream()
+    plans = {}
+    for name, ncomp, eng in (("plan_1", 1, 0), ("plan_1024", 1024, 0), ("plan_8192", 8192, 0),
+                             ("plan_1024_tile", 1024, 1)):
+        comp = hiccl_amd.Compute(torch.float32, device=torch.cuda.current_device(), engine=eng)
+        off = 0
+        for b in range(ncomp):
+            c = count // ncomp + (1 if b < count % ncomp else 0)
+            comp.add([(t, off) for t in ins], (out, off), c, compid=0)
+            off += c
+        plans[name] = comp
+    runs = {"single": lambda: hiccl_amd.reduce(out, ins)}
+    for name, comp in plans.items():
+        runs[name] = (lambda c: (lambda: c.start(stream=stream)))(comp)
+    res = {k: [] for k in runs}
+    for _ in range(3):
+        for k, fn in runs.items():
+            _, ms = time_launches(fn, max(args.steps, 10), args.warmup)
+            res[k].append(float(np.median(ms)))
+    for k, v in res.items():
+        t = float(np.median(v)) * 1e-3
+        eng = plans[k].engine() if k in plans else None
+        print(json.dumps({"mode": "planvs", "run": k, "engine": eng, "kernel_ms": round(t * 1e3, 4),
+                          "GBps": round(9 * count * 4 / t / 1e9, 1)}), flush=True)
+    ok = sample_check(out, n, count)
+    print(json.dumps({"mode": "planvs", "parity_sample_ok": ok}), flush=True)
+    for comp in plans.values():
+        comp.close()
     return 0
 
 

@@ -446,18 +446,49 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_single(SingleArgs a) {
   }
 }
 
+// The plan's device pointer table is read through the constant address space
+// (4): the loads are then scalar (s_load) and the pointers known uniform.
+// Through a generic pointer the compiler emits a flat load -- whose
+// s_waitcnt vmcnt(0) drains every buffer load in flight -- and a
+// readfirstlane waterfall loop around every buffer load using the pointer.
+typedef const char *const __attribute__((address_space(4))) ConstPtr;
+
 struct TableInputs {
   const char *const *p;
-  __device__ const char *operator()(int k) const { return p[k]; }
+  __device__ const char *operator()(int k) const { return ((ConstPtr *)p)[k]; }
 };
 
+// Compute owning global unit t: the c' >= c with desc[c'].tile_begin <= t <
+// desc[c'+1].tile_begin (desc[ncomp] is the sentinel).  Galloping then
+// binary search: ~2 log2(advance) dependent scalar loads (a grid-stride step
+// can skip hundreds of small computes).
+__device__ __forceinline__ uint32_t find_comp(const PlanDesc *__restrict__ desc, uint32_t c,
+                                              uint32_t ncomp, uint64_t t) {
+  if (t < desc[c + 1].tile_begin) return c;
+  uint32_t lo = c + 1, step = 1, hi;
+  while (true) {  // invariant: desc[lo].tile_begin <= t
+    const uint32_t probe = lo + step;
+    if (probe >= ncomp || t < desc[probe].tile_begin) {
+      hi = probe < ncomp ? probe : ncomp;
+      break;
+    }
+    lo = probe;
+    step <<= 1;
+  }
+  while (hi - lo > 1) {  // desc[lo].tile_begin <= t < desc[hi].tile_begin
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (desc[mid].tile_begin <= t) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
 // All computes of a plan in one launch.  Global tile t belongs to compute c
-// with desc[c].tile_begin <= t < desc[c+1].tile_begin (desc[numdesc] is a
+// with desc[c].tile_begin <= t < desc[c+1].tile_begin (desc[ncomp] is a
 // sentinel); c only grows along a workgroup's grid-stride walk.
 template <class Op, int BLOCK, int U, int POL, int ENG>
 __global__ __launch_bounds__(BLOCK) void k_reduce_plan(const PlanDesc *__restrict__ desc,
-                                                       uint32_t c_first, uint64_t t_begin,
-                                                       uint64_t t_end) {
+                                                       uint32_t c_first, uint32_t ncomp,
+                                                       uint64_t t_begin, uint64_t t_end) {
   const int tid = threadIdx.x;
   uint32_t voff[U];
 #pragma unroll
@@ -465,7 +496,7 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_plan(const PlanDesc *__restric
   constexpr uint64_t TILE = (uint64_t)BLOCK * U;
   uint32_t c = c_first;
   for (uint64_t t = t_begin + blockIdx.x; t < t_end; t += gridDim.x) {
-    while (t >= desc[c + 1].tile_begin) c++;
+    c = find_comp(desc, c, ncomp, t);
     const PlanDesc d = desc[c];
     const uint64_t lt = t - d.tile_begin;
     TableInputs raw{d.in};
@@ -821,14 +852,14 @@ uint64_t unit_pkts(int engine, int dtype, int acc) {
                                       : (uint64_t)kPlanBlock * kPlanUnroll;
 }
 
-typedef void (*plan_fn)(const PlanDesc *, uint32_t, uint64_t, uint64_t, dim3, hipStream_t);
+typedef void (*plan_fn)(const PlanDesc *, uint32_t, uint32_t, uint64_t, uint64_t, dim3, hipStream_t);
 
 template <class Op, int ENG>
-void launch_plan_t(const PlanDesc *d, uint32_t c0, uint64_t t0, uint64_t t1, dim3 grid,
+void launch_plan_t(const PlanDesc *d, uint32_t c0, uint32_t ncomp, uint64_t t0, uint64_t t1, dim3 grid,
                    hipStream_t s) {
   constexpr int B = ENG == kPhase ? kPhBlock : kPlanBlock;
   constexpr int U = ENG == kPhase ? phase_p<Op>() : kPlanUnroll;
-  hipLaunchKernelGGL((k_reduce_plan<Op, B, U, kDefPol, ENG>), grid, dim3(B), 0, s, d, c0, t0, t1);
+  hipLaunchKernelGGL((k_reduce_plan<Op, B, U, kDefPol, ENG>), grid, dim3(B), 0, s, d, c0, ncomp, t0, t1);
 }
 
 template <class Op>
@@ -1026,7 +1057,7 @@ int plan_kernel(hiccl_reduce_plan *p, uint32_t c0, uint64_t t0, uint64_t t1, int
   if (!fn) return fail(hipErrorInvalidValue, "plan: unsupported dtype");
   uint64_t grid = (uint64_t)device_cus(p->device) * kPlanBpc;
   if (grid > t1 - t0) grid = t1 - t0;
-  fn(p->d_desc, c0, t0, t1, dim3((unsigned)grid), s);
+  fn(p->d_desc, c0, (uint32_t)p->comps.size(), t0, t1, dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "plan: launch");
 }
 
@@ -1057,7 +1088,7 @@ int reduce_via_table(int dtype, int acc, int engine, void *out, const void *cons
   plan_fn fn = pick_plan(dtype, acc, engine);
   uint64_t grid = (uint64_t)device_cus(current_device()) * kPlanBpc;
   if (grid > tiles) grid = tiles;
-  fn((const PlanDesc *)dmem, 0, 0, tiles, dim3((unsigned)grid), s);
+  fn((const PlanDesc *)dmem, 0, 1, 0, tiles, dim3((unsigned)grid), s);
   if (int e = check_hip(hipGetLastError(), "hiccl_reduce: launch")) return e;
   return check_hip(hipFreeAsync(dmem, s), "hiccl_reduce: hipFreeAsync");
 }

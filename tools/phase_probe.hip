@@ -619,7 +619,7 @@ int pp_run(int kind, int block, int param, int depth, int nt, int grid, const vo
     PN(256, 8, 2) PN(256, 16, 2) PN(512, 8, 2) PN(1024, 4, 2) PN(1024, 8, 2)
     PN(512, 8, 3) PN(1024, 4, 3) PN(512, 4, 3) PN(512, 4, 4) PN(1024, 8, 3) PN(256, 16, 3)
     PN(512, 16, 2) PN(512, 12, 2) PN(512, 14, 2) PN(256, 24, 2) PN(256, 32, 2) PN(256, 36, 2)
-    PN(1024, 6, 2) PN(768, 8, 2)
+    PN(1024, 6, 2) PN(768, 8, 2) PN(512, 16, 1) PN(1024, 8, 1) PN(512, 8, 1)
   } else if (kind == 3) {
     if (block == 512 && param == 16) return launch(k_phase_lds<512, 16>, grid, 512, a, s);
     if (block == 512 && param == 8) return launch(k_phase_lds<512, 8>, grid, 512, a, s);

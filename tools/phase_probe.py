@@ -65,10 +65,8 @@ def main():
     modes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2").split(",")]
     buckets = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     # (kind, block, param, depth, nt, grid); kind 0 phase (runtime n), 1 slab, 2 phase_n (n = 8)
-    variants = [(2, 512, 16, 2, 1, 256), (8, 512, 8, 2, 1, 256), (8, 512, 4, 4, 1, 256),
-                (8, 512, 8, 4, 1, 256), (8, 512, 4, 8, 1, 256), (8, 1024, 4, 2, 1, 256),
-                (8, 1024, 4, 4, 1, 256), (8, 256, 8, 8, 1, 256), (8, 512, 6, 4, 1, 256),
-                (2, 512, 16, 2, 1, 256)]
+    variants = [(2, 512, 16, 2, 1, 256), (2, 512, 16, 1, 1, 256), (2, 1024, 8, 1, 1, 256),
+                (2, 512, 8, 1, 1, 256), (2, 512, 8, 1, 1, 512), (2, 512, 16, 2, 1, 256)]
     g = P.pp_granularity()
     print(json.dumps({"vmm_granularity_min": g >> 32, "vmm_granularity_rec": g & 0xffffffff}), flush=True)
     stream = torch.cuda.current_stream()
