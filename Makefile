@@ -14,8 +14,13 @@ all: $(LIB) $(PROBE) cpp oracle
 $(PROBE): tools/hbm_probe.hip
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
+# The atomic optimizer rewrites the one-lane unit-ticket grab into a
+# wave-reduction whose result is read back at once (s_waitcnt vmcnt(0) at the
+# top of every unit); without it the wait lands after the unit's last add.
+LIBFLAGS = -mllvm -amdgpu-atomic-optimizer-strategy=None
+
 $(LIB): hiccl_amd/csrc/reduce.hip include/hiccl_reduce.h
-	$(HIPCC) $(HIPFLAGS) -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(LIBFLAGS) -o $@ $<
 
 oracle:
 	$(MAKE) -C oracle

@@ -32,6 +32,10 @@ HICCL_ENGINE_AUTO = 0
 HICCL_ENGINE_TILE = 1
 HICCL_ENGINE_PHASE = 2
 
+HICCL_SCHED_AUTO = 0
+HICCL_SCHED_STATIC = 1
+HICCL_SCHED_DYNAMIC = 2
+
 DTYPE_OF_TORCH = {
     torch.float32: HICCL_FLOAT32,
     torch.float64: HICCL_FLOAT64,
@@ -54,7 +58,7 @@ class ReduceConfig(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("unroll", ctypes.c_int),
                 ("blocks_per_cu", ctypes.c_int), ("nontemporal", ctypes.c_int),
                 ("acc", ctypes.c_int), ("grid", ctypes.c_int), ("store_policy", ctypes.c_int),
-                ("engine", ctypes.c_int)]
+                ("engine", ctypes.c_int), ("schedule", ctypes.c_int)]
 
 
 _lib = None

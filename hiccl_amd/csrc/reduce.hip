@@ -30,6 +30,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <map>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -262,6 +263,7 @@ struct SingleArgs {
   uint32_t head;      // scalar elements before the body
   uint32_t tail;      // scalar elements after the body
   uint32_t pad;
+  uint32_t *sched;    // dynamic unit counter {ticket, done}, or NULL: static grid-stride
   const char *in[kMaxArgInputs];
 };
 
@@ -319,9 +321,17 @@ __device__ __forceinline__ void group_at(typename Op::acc_t (&acc)[U], Inputs in
 // tile (< the full tile only for the last one).  Inputs are consumed as full
 // groups of 8 followed by one statically sized remainder group, so the adds
 // happen in exactly the order k = 0, 1, ..., n-1.
-template <class Op, int U, int POL, class Inputs>
+// `before_store()` runs after the last add, before the stores (the unit
+// scheduler publishes its next ticket there: every load has been waited for
+// and no store is pending yet, so reading the atomic's result costs nothing).
+struct NoHook {
+  __device__ void operator()() const {}
+};
+
+template <class Op, int U, int POL, class Inputs, class Hook = NoHook>
 __device__ __forceinline__ void tile_body(char *outb, Inputs in, uint32_t n, uint64_t tile_off,
-                                          uint32_t tile_bytes, const uint32_t (&voff)[U]) {
+                                          uint32_t tile_bytes, const uint32_t (&voff)[U],
+                                          Hook before_store = Hook()) {
   typename Op::acc_t acc[U];
 #pragma unroll
   for (int u = 0; u < U; u++) acc[u] = Op::zero();
@@ -337,6 +347,7 @@ __device__ __forceinline__ void tile_body(char *outb, Inputs in, uint32_t n, uin
     case 7: group_at<Op, U, 7, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
     default: break;
   }
+  before_store();
   rsrc_t w = make_rsrc(outb + tile_off, tile_bytes);
 #pragma unroll
   for (int u = 0; u < U; u++) store_pkt<POL>(w, voff[u], Op::pack(acc[u]));
@@ -354,9 +365,10 @@ __device__ __forceinline__ void tile_body(char *outb, Inputs in, uint32_t n, uin
 // n is runtime: inputs are taken in pairs; the load that would read past
 // input n-1 gets a zero-range descriptor (no memory traffic, reads 0, never
 // added).
-template <class Op, int P, int POL, class Inputs>
+template <class Op, int P, int POL, class Inputs, class Hook = NoHook>
 __device__ __forceinline__ void chunk_body(char *outb, Inputs in, uint32_t n, uint64_t off,
-                                           uint32_t nbytes, const uint32_t (&voff)[P]) {
+                                           uint32_t nbytes, const uint32_t (&voff)[P],
+                                           Hook before_store = Hook()) {
   typename Op::acc_t acc[P];
 #pragma unroll
   for (int p = 0; p < P; p++) acc[p] = Op::zero();
@@ -396,6 +408,7 @@ __device__ __forceinline__ void chunk_body(char *outb, Inputs in, uint32_t n, ui
       for (int p = 0; p < P; p++) acc[p] = Op::add(acc[p], x[p]);
     }
   }
+  before_store();
   rsrc_t w = make_rsrc(outb + off, nbytes);
 #pragma unroll
   for (int p = 0; p < P; p++) store_pkt<POL>(w, voff[p], Op::pack(acc[p]));
@@ -406,13 +419,13 @@ __device__ __forceinline__ void chunk_body(char *outb, Inputs in, uint32_t n, ui
 constexpr int kTile = 0;
 constexpr int kPhase = 1;
 
-template <class Op, int U, int POL, int ENG, class Inputs>
+template <class Op, int U, int POL, int ENG, class Inputs, class Hook>
 __device__ __forceinline__ void unit_body(char *outb, Inputs in, uint32_t n, uint64_t off,
-                                          uint32_t nbytes, const uint32_t (&voff)[U]) {
+                                          uint32_t nbytes, const uint32_t (&voff)[U], Hook hook) {
   if constexpr (ENG == kPhase)
-    chunk_body<Op, U, POL>(outb, in, n, off, nbytes, voff);
+    chunk_body<Op, U, POL>(outb, in, n, off, nbytes, voff, hook);
   else
-    tile_body<Op, U, POL>(outb, in, n, off, nbytes, voff);
+    tile_body<Op, U, POL>(outb, in, n, off, nbytes, voff, hook);
 }
 
 // Body inputs shifted by the head: base(k) = in[k] + head*esz.
@@ -422,6 +435,55 @@ struct Shifted {
   uint64_t shift;
   __device__ const char *operator()(int k) const { return in(k) + shift; }
 };
+
+// ---------------------------------------------------- unit scheduling ----
+//
+// Static: workgroup b takes units b, b + grid, ...  Dynamic (sched != NULL):
+// every workgroup takes its next unit from a device counter, so the
+// workgroups the memory system serves faster do more units and the launch's
+// tail is one unit instead of the slowest workgroup's share (+1.6-2.1 % on
+// C2: profiles/r01_phase_probe_dyn.jsonl).  The next ticket is fetched one
+// unit ahead so the atomic's latency hides under the current unit.  The
+// counter pair {ticket, done} is zero on entry; the last workgroup to finish
+// resets it, so consecutive launches on one stream (or replays of a graph)
+// reuse it without a memset.  The host gives every (device, stream) its own
+// pair and never uses it during stream capture (unit_sched_for()).
+template <class Body>
+__device__ __forceinline__ void for_each_unit(uint32_t *sched, uint64_t t0, uint64_t t1, Body body) {
+  if (!sched) {
+    for (uint64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) body(t, NoHook());
+    return;
+  }
+  __shared__ uint32_t s_next[2];
+  if (threadIdx.x == 0)
+    s_next[0] = __hip_atomic_fetch_add(&sched[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  uint64_t t = t0 + s_next[0];
+  int slot = 1;
+  while (t < t1) {
+    // the grab is issued before the unit's loads; its value is published
+    // after the unit's last add and before its stores (the body's hook):
+    // all loads have been waited for by then and no store is pending, so the
+    // wait costs nothing (a wait with stores pending would be vmcnt(0))
+    uint32_t nxt;  // meaningful in lane 0 only; no merge value, so no wait at the branch join
+    if (threadIdx.x == 0)
+      nxt = __hip_atomic_fetch_add(&sched[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    body(t, [&]() {
+      if (threadIdx.x == 0) s_next[slot] = nxt;
+    });
+    __syncthreads();
+    t = t0 + s_next[slot];
+    slot ^= 1;
+  }
+  if (threadIdx.x == 0) {
+    // every ticket grab of this workgroup precedes its done increment
+    const uint32_t prev = __hip_atomic_fetch_add(&sched[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {  // last workgroup: no grab is outstanding
+      __hip_atomic_store(&sched[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sched[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 
 // ------------------------------------------------------------ kernels ------
 
@@ -433,17 +495,17 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_single(SingleArgs a) {
   for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * BLOCK + tid) * kPacket);
   ArgInputs raw{a.in};
   if (blockIdx.x == 0) scalar_part<Op>(a.out, raw, a.n, a.head, a.npkt, a.tail, tid);
-  if (a.npkt == 0) return;
+  if (a.npkt == 0) return;  // (the host never passes a sched counter then)
   const uint64_t shift = (uint64_t)a.head * Op::kEsz;
   Shifted<ArgInputs> in{raw, shift};
   char *outb = a.out + shift;
   constexpr uint64_t TILE = (uint64_t)BLOCK * U;
-  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+  for_each_unit(a.sched, 0, a.ntiles, [&](uint64_t t, auto hook) {
     const uint64_t pkt0 = t * TILE;
     const uint64_t left = a.npkt - pkt0;
     const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
-    unit_body<Op, U, POL, ENG>(outb, in, a.n, pkt0 * kPacket, tile_bytes, voff);
-  }
+    unit_body<Op, U, POL, ENG>(outb, in, a.n, pkt0 * kPacket, tile_bytes, voff, hook);
+  });
 }
 
 // The plan's device pointer table is read through the constant address space
@@ -488,27 +550,31 @@ __device__ __forceinline__ uint32_t find_comp(const PlanDesc *__restrict__ desc,
 template <class Op, int BLOCK, int U, int POL, int ENG>
 __global__ __launch_bounds__(BLOCK) void k_reduce_plan(const PlanDesc *__restrict__ desc,
                                                        uint32_t c_first, uint32_t ncomp,
-                                                       uint64_t t_begin, uint64_t t_end) {
+                                                       uint64_t t_begin, uint64_t t_end,
+                                                       uint32_t *sched) {
   const int tid = threadIdx.x;
   uint32_t voff[U];
 #pragma unroll
   for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * BLOCK + tid) * kPacket);
   constexpr uint64_t TILE = (uint64_t)BLOCK * U;
-  uint32_t c = c_first;
-  for (uint64_t t = t_begin + blockIdx.x; t < t_end; t += gridDim.x) {
+  uint32_t c = c_first;  // units arrive in increasing order (static or dynamic)
+  for_each_unit(sched, t_begin, t_end, [&](uint64_t t, auto hook) {
     c = find_comp(desc, c, ncomp, t);
     const PlanDesc d = desc[c];
     const uint64_t lt = t - d.tile_begin;
     TableInputs raw{d.in};
     if (lt == 0) scalar_part<Op>(d.out, raw, d.n, d.head, d.npkt, d.tail, tid);
     const uint64_t pkt0 = lt * TILE;
-    if (pkt0 >= d.npkt) continue;
+    if (pkt0 >= d.npkt) {  // a scalar-only compute: nothing to load or store
+      hook();
+      return;
+    }
     const uint64_t shift = (uint64_t)d.head * Op::kEsz;
     Shifted<TableInputs> in{raw, shift};
     const uint64_t left = d.npkt - pkt0;
     const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
-    unit_body<Op, U, POL, ENG>(d.out + shift, in, d.n, pkt0 * kPacket, tile_bytes, voff);
-  }
+    unit_body<Op, U, POL, ENG>(d.out + shift, in, d.n, pkt0 * kPacket, tile_bytes, voff, hook);
+  });
 }
 
 // ------------------------------------------------------- synthetic inputs --
@@ -616,6 +682,43 @@ int device_cus(int dev) {
   return g_dev[dev].cus;
 }
 
+// Dynamic-scheduling counter pairs, one per (device, stream), allocated on
+// first use (64 B apart) and zeroed once; the kernels leave them zero.
+struct SchedKey {
+  int dev;
+  hipStream_t s;
+  bool operator<(const SchedKey &o) const { return dev != o.dev ? dev < o.dev : s < o.s; }
+};
+std::mutex g_sched_mu;
+std::map<SchedKey, uint32_t *> g_sched;
+
+// Units per workgroup below which a dynamic schedule cannot pay off.
+constexpr uint64_t kDynMinUnitsPerWG = 4;
+
+// The counter pair for a launch of `units` work units on `grid` workgroups
+// of the PHASE engine on (dev, s), or NULL for a static schedule (TILE
+// engine, few units, stream capture -- a replayed graph could run beside
+// other work on the same stream's counter -- or any allocation failure).
+uint32_t *unit_sched_for(int engine, uint64_t units, uint64_t grid, int dev, hipStream_t s,
+                         int schedule = HICCL_SCHED_AUTO) {
+  if (schedule == HICCL_SCHED_STATIC) return nullptr;
+  if (schedule == HICCL_SCHED_AUTO && engine != HICCL_ENGINE_PHASE) return nullptr;
+  if (units < kDynMinUnitsPerWG * grid) return nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
+  std::lock_guard<std::mutex> lk(g_sched_mu);
+  auto it = g_sched.find(SchedKey{dev, s});
+  if (it != g_sched.end()) return it->second;
+  uint32_t *p = nullptr;
+  if (hipMalloc((void **)&p, 64) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, 64) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  g_sched[SchedKey{dev, s}] = p;
+  return p;
+}
+
 int current_device() {
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess) d = 0;
@@ -707,12 +810,12 @@ int phase_p_dtype(int dtype, int acc) {
 }
 
 struct Cfg {
-  int block, unroll, bpc, nt, acc, grid, store, engine;
+  int block, unroll, bpc, nt, acc, grid, store, engine, schedule;
 };
 
 // Raw config: zero block/unroll stay zero until the engine is known.
 Cfg resolve(const hiccl_reduce_config_t *c) {
-  Cfg r{0, 0, kDefBpc, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO};
+  Cfg r{0, 0, kDefBpc, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO, HICCL_SCHED_AUTO};
   if (c) {
     r.block = c->block;
     r.unroll = c->unroll;
@@ -722,6 +825,7 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
     r.grid = c->grid;
     if (c->store_policy) r.store = c->store_policy - 1;
     r.engine = c->engine;
+    r.schedule = c->schedule;
   }
   return r;
 }
@@ -852,14 +956,16 @@ uint64_t unit_pkts(int engine, int dtype, int acc) {
                                       : (uint64_t)kPlanBlock * kPlanUnroll;
 }
 
-typedef void (*plan_fn)(const PlanDesc *, uint32_t, uint32_t, uint64_t, uint64_t, dim3, hipStream_t);
+typedef void (*plan_fn)(const PlanDesc *, uint32_t, uint32_t, uint64_t, uint64_t, uint32_t *, dim3,
+                        hipStream_t);
 
 template <class Op, int ENG>
-void launch_plan_t(const PlanDesc *d, uint32_t c0, uint32_t ncomp, uint64_t t0, uint64_t t1, dim3 grid,
-                   hipStream_t s) {
+void launch_plan_t(const PlanDesc *d, uint32_t c0, uint32_t ncomp, uint64_t t0, uint64_t t1,
+                   uint32_t *sched, dim3 grid, hipStream_t s) {
   constexpr int B = ENG == kPhase ? kPhBlock : kPlanBlock;
   constexpr int U = ENG == kPhase ? phase_p<Op>() : kPlanUnroll;
-  hipLaunchKernelGGL((k_reduce_plan<Op, B, U, kDefPol, ENG>), grid, dim3(B), 0, s, d, c0, ncomp, t0, t1);
+  hipLaunchKernelGGL((k_reduce_plan<Op, B, U, kDefPol, ENG>), grid, dim3(B), 0, s, d, c0, ncomp, t0, t1,
+                     sched);
 }
 
 template <class Op>
@@ -916,6 +1022,8 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
     return fail(hipErrorInvalidValue, "hiccl_reduce: bad acc mode");
   if (c.engine < HICCL_ENGINE_AUTO || c.engine > HICCL_ENGINE_PHASE)
     return fail(hipErrorInvalidValue, "hiccl_reduce: bad engine");
+  if (c.schedule < HICCL_SCHED_AUTO || c.schedule > HICCL_SCHED_DYNAMIC)
+    return fail(hipErrorInvalidValue, "hiccl_reduce: bad schedule");
   hipStream_t s = (hipStream_t)stream;
   const int dev = current_device();
   Split sp = split_on(out, count, esz);
@@ -946,6 +1054,7 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
 
   uint64_t grid = c.grid > 0 ? (uint64_t)c.grid : (uint64_t)device_cus(dev) * c.bpc;
   if (grid > a.ntiles) grid = a.ntiles;
+  a.sched = unit_sched_for(c.engine, a.ntiles, grid, dev, s, c.schedule);
   fn(a, dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "hiccl_reduce: launch");
 }
@@ -1057,7 +1166,8 @@ int plan_kernel(hiccl_reduce_plan *p, uint32_t c0, uint64_t t0, uint64_t t1, int
   if (!fn) return fail(hipErrorInvalidValue, "plan: unsupported dtype");
   uint64_t grid = (uint64_t)device_cus(p->device) * kPlanBpc;
   if (grid > t1 - t0) grid = t1 - t0;
-  fn(p->d_desc, c0, (uint32_t)p->comps.size(), t0, t1, dim3((unsigned)grid), s);
+  fn(p->d_desc, c0, (uint32_t)p->comps.size(), t0, t1,
+     unit_sched_for(p->engine, t1 - t0, grid, p->device, s), dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "plan: launch");
 }
 
@@ -1088,7 +1198,8 @@ int reduce_via_table(int dtype, int acc, int engine, void *out, const void *cons
   plan_fn fn = pick_plan(dtype, acc, engine);
   uint64_t grid = (uint64_t)device_cus(current_device()) * kPlanBpc;
   if (grid > tiles) grid = tiles;
-  fn((const PlanDesc *)dmem, 0, 1, 0, tiles, dim3((unsigned)grid), s);
+  fn((const PlanDesc *)dmem, 0, 1, 0, tiles, unit_sched_for(engine, tiles, grid, current_device(), s),
+     dim3((unsigned)grid), s);
   if (int e = check_hip(hipGetLastError(), "hiccl_reduce: launch")) return e;
   return check_hip(hipFreeAsync(dmem, s), "hiccl_reduce: hipFreeAsync");
 }

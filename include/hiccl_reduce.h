@@ -65,6 +65,20 @@ typedef enum {
   HICCL_ENGINE_PHASE = 2
 } hiccl_engine_t;
 
+/* Work-unit schedule (same bits either way).
+ *   STATIC   workgroup b takes units b, b + grid, ...
+ *   DYNAMIC  workgroups take their next unit from a device counter (one per
+ *            device and stream, reset by the launch itself): faster-served
+ *            workgroups do more units, the tail is one unit.
+ *   AUTO     DYNAMIC for the PHASE engine with >= 4 units per workgroup,
+ *            STATIC otherwise and always during stream capture.
+ * Plans use AUTO. */
+typedef enum {
+  HICCL_SCHED_AUTO = 0,
+  HICCL_SCHED_STATIC = 1,
+  HICCL_SCHED_DYNAMIC = 2
+} hiccl_schedule_t;
+
 /* Size in bytes of one element of `dtype`, 0 if unknown. */
 size_t hiccl_dtype_size(int dtype);
 
@@ -107,6 +121,7 @@ typedef struct {
   int grid;          /* total workgroups; overrides blocks_per_cu when > 0 */
   int store_policy;  /* stores: 1 plain, 2 nt, 3 sc1 (write-through, line dropped from L2) */
   int engine;        /* hiccl_engine_t */
+  int schedule;      /* hiccl_schedule_t */
 } hiccl_reduce_config_t;
 
 int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t count,

@@ -155,12 +155,72 @@ def test_phase_variants_same_bits(oracle, config):
             assert bits_equal(gotb, oracle.reduce(list(xb), dtype=np.uint16)), config
 
 
+@pytest.mark.parametrize("engine", [1, 2], ids=["tile", "phase"])
+@pytest.mark.parametrize("grid", [4, 16])
+def test_dynamic_schedule_same_bits(oracle, engine, grid):
+    """Dynamic unit scheduling (device ticket counter, reset by the launch
+    itself) against static, repeated launches on one stream (the counter
+    must come back to zero each time: a stale counter would skip units and
+    leave the NaN prefill), and a second stream (its own counter)."""
+    S = hiccl_amd._lib
+    for n, count in ((8, (1 << 20) + 5), (3, 777777)):
+        x = oracle.fill(n, count, seed=n + grid)
+        exp = oracle.reduce(list(x))
+        ins = [to_dev(r) for r in x]
+        out = torch.empty(count, device=DEV)
+        side = torch.cuda.Stream()
+        for sched in (S.HICCL_SCHED_STATIC, S.HICCL_SCHED_DYNAMIC):
+            cfg = dict(engine=engine, grid=grid, schedule=sched)
+            for rep in range(5):
+                out.fill_(float("nan"))
+                hiccl_amd.reduce(out, ins, config=cfg)
+                torch.cuda.synchronize()
+                got = out.cpu().numpy()
+                assert bits_equal(got, exp), (sched, rep, first_mismatch(got, exp))
+            side.wait_stream(torch.cuda.current_stream())
+            out.fill_(float("nan"))
+            torch.cuda.current_stream().synchronize()
+            hiccl_amd.reduce(out, ins, config=cfg, stream=side)
+            side.synchronize()
+            got = out.cpu().numpy()
+            assert bits_equal(got, exp), (sched, "side stream", first_mismatch(got, exp))
+
+
+def test_dynamic_schedule_plan_many_computes(oracle):
+    """A phased plan big enough for the dynamic schedule (>= 4 units per
+    workgroup), many computes of ragged sizes, launched 3 times."""
+    rng = np.random.default_rng(11)
+    comp = hiccl_amd.Compute(torch.float32, device=0, engine=hiccl_amd.HICCL_ENGINE_PHASE)
+    outs, exps, keep = [], [], []
+    for c in range(300):
+        n = int(rng.integers(1, 9))
+        count = int(rng.integers(1, 400000))  # ~2,000 units of 128 KiB: dynamic
+        x = oracle.fill(n, count, seed=500 + c)
+        ins = [to_dev(r) for r in x]
+        keep += ins
+        out = torch.empty(count, device=DEV)
+        comp.add(ins, out, count, compid=0)
+        outs.append(out)
+        exps.append(oracle.reduce(list(x)))
+    for _ in range(3):
+        for o in outs:
+            o.fill_(float("nan"))
+        comp.start()
+        comp.wait()
+        for o, e in zip(outs, exps):
+            got = o.cpu().numpy()
+            assert bits_equal(got, e), first_mismatch(got, e)
+    comp.close()
+
+
 def test_phase_unsupported_shape_is_an_error():
     x = torch.zeros(100, device=DEV)
     with pytest.raises(hiccl_amd.HicclError):
         hiccl_amd.reduce(x, [x, x], config=dict(engine=2, block=128, unroll=16))
     with pytest.raises(hiccl_amd.HicclError):
         hiccl_amd.reduce(x, [x, x], config=dict(engine=7))
+    with pytest.raises(hiccl_amd.HicclError):
+        hiccl_amd.reduce(x, [x, x], config=dict(schedule=9))
 
 
 @pytest.mark.parametrize("config", [
