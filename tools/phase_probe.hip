@@ -547,6 +547,69 @@ __global__ __launch_bounds__(B) void k_phase_q(PArgs a) {
   }
 }
 
+// Phased (N = 8, D = 2) with DYNAMIC chunk assignment: each workgroup takes
+// its next chunk from a device counter (zeroed per launch), so workgroups the
+// memory system serves faster do more chunks and the kernel's tail is one
+// chunk, not the slowest workgroup's share.  The next index is fetched one
+// chunk ahead (the atomic's latency hides under the current chunk).
+template <int B, int P>
+__global__ __launch_bounds__(B) void k_phase_dyn(PArgs a, unsigned int *counter) {
+  constexpr int N = 8;
+  constexpr uint64_t CH = (uint64_t)B * P * 16;
+  const uint64_t nch = (a.bytes + CH - 1) / CH;
+  uint32_t voff[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) voff[p] = (uint32_t)((p * B + threadIdx.x) * 16);
+  __shared__ unsigned int next_c[2];
+  if (threadIdx.x == 0) {
+    next_c[0] = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  uint64_t c = next_c[0];
+  int slot = 1;
+  while (c < nch) {
+    if (threadIdx.x == 0)
+      next_c[slot] = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t off = c * CH;
+    const uint32_t nb = (uint32_t)((a.bytes - off) < CH ? (a.bytes - off) : CH);
+    f32x4 acc[P], x[2][P];
+#pragma unroll
+    for (int p = 0; p < P; p++) acc[p] = (f32x4)(0.0f);
+    {
+      rsrc_t r = mk(a.in[0] + off, nb);
+#pragma unroll
+      for (int p = 0; p < P; p++) x[0][p] = ld<2>(r, voff[p]);
+    }
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      if (j + 1 < N) {
+        rsrc_t r = mk(a.in[j + 1] + off, nb);
+#pragma unroll
+        for (int p = 0; p < P; p++) x[(j + 1) & 1][p] = ld<2>(r, voff[p]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int p = 0; p < P; p++) acc[p] += x[j & 1][p];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    rsrc_t w = mk(a.out + off, nb);
+#pragma unroll
+    for (int p = 0; p < P; p++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[p]), w, (int)voff[p], 0, 2);
+    __syncthreads();
+    c = next_c[slot];
+    slot ^= 1;
+  }
+}
+
+template <int B, int P>
+static int launch_dyn(int grid, const PArgs &a, hipStream_t s) {
+  unsigned int *ctr = sync_counter();
+  if (hipMemsetAsync(ctr, 0, sizeof(unsigned int), s)) return -5;
+  hipLaunchKernelGGL((k_phase_dyn<B, P>), dim3(grid), dim3(B), 0, s, a, ctr);
+  return (int)hipGetLastError();
+}
+
 // Product tile order (all n inputs of a tile loaded together), slab-walked.
 template <int B, int U, int AUXL, int AUXS>
 __global__ __launch_bounds__(B) void k_slab(PArgs a) {
@@ -647,6 +710,11 @@ int pp_run(int kind, int block, int param, int depth, int nt, int grid, const vo
     if (block == 1024 && param == 4 && depth == 4) return launch(k_phase_q<1024, 4, 4>, grid, 1024, a, s);
     if (block == 256 && param == 8 && depth == 8) return launch(k_phase_q<256, 8, 8>, grid, 256, a, s);
     if (block == 512 && param == 6 && depth == 4) return launch(k_phase_q<512, 6, 4>, grid, 512, a, s);
+  } else if (kind == 9) {
+    if (n != 8) return -3;
+    if (block == 512 && param == 16) return launch_dyn<512, 16>(grid, a, s);
+    if (block == 1024 && param == 8) return launch_dyn<1024, 8>(grid, a, s);
+    if (block == 512 && param == 8) return launch_dyn<512, 8>(grid, a, s);
   } else if (kind == 4) {  // depth = MODE
     if (n != 8) return -3;
     if (block == 512 && param == 16 && depth == 0) return launch(k_phase_x<512, 16, 0>, grid, 512, a, s);
