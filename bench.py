@@ -268,9 +268,10 @@ def sample_check(out, n, count, bf16=False, seed=SEED, nsample=1024):
     return bool(np.array_equal(got.view(np.uint8), exp.view(np.uint8)))
 
 
-# The kernel the default (auto) config runs on C2: the phased engine's f32
-# default shape (hiccl_amd/csrc/reduce.hip: 512 lanes x 16 packets, nt/nt).
-DEFAULT_KERNEL = "OpF32, 512, 16, 11, 1>"
+# The kernel the default (auto) config runs on C2: the tile engine's f32
+# default shape on the dynamic schedule (hiccl_amd/csrc/reduce.hip: 256
+# lanes x 4 packets, nt/nt).
+DEFAULT_KERNEL = "OpF32, 256, 4, 11, 0>"
 
 
 def traffic_from_profiles(n, count, kernel=DEFAULT_KERNEL):
@@ -317,6 +318,8 @@ def main():
     ap.add_argument("--c2variants", action="store_true")
     ap.add_argument("--crossover", action="store_true")
     ap.add_argument("--planvs", action="store_true")
+    ap.add_argument("--schedsweep", action="store_true")
+    ap.add_argument("--buckets", type=int, default=0, help="schedsweep: this many fresh --n x 2^--log2count buckets")
     args = ap.parse_args()
 
     dist = Dist(args.gpus)
@@ -332,6 +335,8 @@ def main():
         return crossover(args)
     if args.planvs:
         return planvs(args)
+    if args.schedsweep:
+        return schedsweep(args)
     if args.roundtrip:
         return roundtrip(args)
 
@@ -485,6 +490,38 @@ def nway(args):
                           "frac_of_copy": round(b / t / 1e9 / copy_gbps, 4)}), flush=True)
       del ins, out
       torch.cuda.empty_cache()
+    return 0
+
+
+def schedsweep(args):
+    """Static vs dynamic unit schedule (and grab size) for both engines,
+    fp32, interleaved rounds.  Default cases n = 2/4/8/16 at 256 MiB and
+    1 GiB per input; --n N --log2count L: that shape on 3 fresh buckets."""
+    cases = ((2, 256), (2, 1024), (4, 256), (4, 1024), (8, 256), (8, 1024), (16, 256))
+    if args.buckets:
+        cases = ((args.n, (1 << args.log2count) * 4 >> 20),) * args.buckets
+    variants = [("tile_static", dict(engine=1, schedule=1)), ("tile_dyn_g1", dict(engine=1, schedule=2, grab=1)),
+                ("tile512_dyn_g1", dict(engine=1, schedule=2, grab=1, block=512, unroll=4)),
+                ("tile_dyn_g2", dict(engine=1, schedule=2, grab=2)),
+                ("phase_static", dict(engine=2, schedule=1)), ("phase_dyn_g1", dict(engine=2, schedule=2, grab=1)),
+                ("auto", None)]
+    for n, mib in cases:
+        count = (mib << 20) // 4
+        ins, out = make_bucket(n, count)
+        res = {}
+        for rnd in range(5):
+            for name, cfg in variants:
+                _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins, config=cfg), max(args.steps, 10),
+                                      args.warmup)
+                res.setdefault(name, []).append(float(np.median(ms)))
+        row = {"mode": "schedsweep", "n": n, "mib_per_input": mib}
+        for name, v in res.items():
+            t = float(np.median(v)) * 1e-3
+            row[name] = round((n + 1) * count * 4 / t / 1e9, 1)
+        row["parity_sample_ok"] = sample_check(out, n, count)
+        print(json.dumps(row), flush=True)
+        del ins, out
+        torch.cuda.empty_cache()
     return 0
 
 

@@ -58,7 +58,8 @@ class ReduceConfig(ctypes.Structure):
     _fields_ = [("block", ctypes.c_int), ("unroll", ctypes.c_int),
                 ("blocks_per_cu", ctypes.c_int), ("nontemporal", ctypes.c_int),
                 ("acc", ctypes.c_int), ("grid", ctypes.c_int), ("store_policy", ctypes.c_int),
-                ("engine", ctypes.c_int), ("schedule", ctypes.c_int)]
+                ("engine", ctypes.c_int), ("schedule", ctypes.c_int), ("grab", ctypes.c_int),
+                ("drain", ctypes.c_int)]
 
 
 _lib = None

@@ -264,6 +264,8 @@ struct SingleArgs {
   uint32_t tail;      // scalar elements after the body
   uint32_t pad;
   uint32_t *sched;    // dynamic unit counter {ticket, done}, or NULL: static grid-stride
+  uint32_t grab;      // units per ticket (dynamic schedule), >= 1
+  uint32_t drain;     // 1: wait for a unit's stores before the next unit's loads
   const char *in[kMaxArgInputs];
 };
 
@@ -448,31 +450,45 @@ struct Shifted {
 // resets it, so consecutive launches on one stream (or replays of a graph)
 // reuse it without a memset.  The host gives every (device, stream) its own
 // pair and never uses it during stream capture (unit_sched_for()).
+__device__ __forceinline__ void drain_stores(uint32_t drain) {
+  if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <class Body>
-__device__ __forceinline__ void for_each_unit(uint32_t *sched, uint64_t t0, uint64_t t1, Body body) {
+__device__ __forceinline__ void for_each_unit(uint32_t *sched, uint32_t grab, uint64_t t0, uint64_t t1,
+                                              Body body, uint32_t drain = 0) {
   if (!sched) {
-    for (uint64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) body(t, NoHook());
+    for (uint64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
+      body(t, [] {});
+      drain_stores(drain);
+    }
     return;
   }
+  // a ticket k covers units [t0 + k*grab, t0 + (k+1)*grab)
   __shared__ uint32_t s_next[2];
   if (threadIdx.x == 0)
     s_next[0] = __hip_atomic_fetch_add(&sched[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  uint64_t t = t0 + s_next[0];
+  uint64_t t = t0 + (uint64_t)s_next[0] * grab;
   int slot = 1;
   while (t < t1) {
-    // the grab is issued before the unit's loads; its value is published
-    // after the unit's last add and before its stores (the body's hook):
-    // all loads have been waited for by then and no store is pending, so the
-    // wait costs nothing (a wait with stores pending would be vmcnt(0))
+    // the next ticket is grabbed before this one's loads; its value is
+    // published after the last unit's last add and before that unit's stores
+    // (the body's hook), where every load has been waited for, so the wait
+    // costs little (a wait with stores pending is vmcnt(0))
     uint32_t nxt;  // meaningful in lane 0 only; no merge value, so no wait at the branch join
     if (threadIdx.x == 0)
       nxt = __hip_atomic_fetch_add(&sched[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    body(t, [&]() {
-      if (threadIdx.x == 0) s_next[slot] = nxt;
-    });
+    const uint64_t tend = (t + grab < t1) ? t + grab : t1;
+    for (uint64_t u = t; u < tend; u++) {
+      const bool last = u + 1 == tend;
+      body(u, [&]() {
+        if (last && threadIdx.x == 0) s_next[slot] = nxt;
+      });
+      drain_stores(drain);
+    }
     __syncthreads();
-    t = t0 + s_next[slot];
+    t = t0 + (uint64_t)s_next[slot] * grab;
     slot ^= 1;
   }
   if (threadIdx.x == 0) {
@@ -500,12 +516,12 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_single(SingleArgs a) {
   Shifted<ArgInputs> in{raw, shift};
   char *outb = a.out + shift;
   constexpr uint64_t TILE = (uint64_t)BLOCK * U;
-  for_each_unit(a.sched, 0, a.ntiles, [&](uint64_t t, auto hook) {
+  for_each_unit(a.sched, a.grab, 0, a.ntiles, [&](uint64_t t, auto hook) {
     const uint64_t pkt0 = t * TILE;
     const uint64_t left = a.npkt - pkt0;
     const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
     unit_body<Op, U, POL, ENG>(outb, in, a.n, pkt0 * kPacket, tile_bytes, voff, hook);
-  });
+  }, a.drain);
 }
 
 // The plan's device pointer table is read through the constant address space
@@ -551,14 +567,14 @@ template <class Op, int BLOCK, int U, int POL, int ENG>
 __global__ __launch_bounds__(BLOCK) void k_reduce_plan(const PlanDesc *__restrict__ desc,
                                                        uint32_t c_first, uint32_t ncomp,
                                                        uint64_t t_begin, uint64_t t_end,
-                                                       uint32_t *sched) {
+                                                       uint32_t *sched, uint32_t grab) {
   const int tid = threadIdx.x;
   uint32_t voff[U];
 #pragma unroll
   for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * BLOCK + tid) * kPacket);
   constexpr uint64_t TILE = (uint64_t)BLOCK * U;
   uint32_t c = c_first;  // units arrive in increasing order (static or dynamic)
-  for_each_unit(sched, t_begin, t_end, [&](uint64_t t, auto hook) {
+  for_each_unit(sched, grab, t_begin, t_end, [&](uint64_t t, auto hook) {
     c = find_comp(desc, c, ncomp, t);
     const PlanDesc d = desc[c];
     const uint64_t lt = t - d.tile_begin;
@@ -692,18 +708,39 @@ struct SchedKey {
 std::mutex g_sched_mu;
 std::map<SchedKey, uint32_t *> g_sched;
 
-// Units per workgroup below which a dynamic schedule cannot pay off.
-constexpr uint64_t kDynMinUnitsPerWG = 4;
+// Tickets per workgroup below which a dynamic schedule does not pay off
+// (C4 at 16 / 64 MiB per input: 4 / 16 tickets per workgroup lose 33 / 14 %
+// to the per-ticket barrier; 64 tickets at 256 MiB gain 3 %).
+constexpr uint64_t kDynMinUnitsPerWG = 32;
+// AUTO schedules dynamically from this many inputs on (TILE engine).
+constexpr double kDynMinInputs = 5;
+// A ticket should cover at least this many 16 KiB input tiles of traffic
+// ((n + 1) per tile): one tile at n >= 8, two at n = 4..7, ... -- a ticket
+// costs an atomic and a workgroup barrier (profiles/r01_schedsweep*.jsonl).
+constexpr double kTicketTiles = 9;
 
-// The counter pair for a launch of `units` work units on `grid` workgroups
-// of the PHASE engine on (dev, s), or NULL for a static schedule (TILE
-// engine, few units, stream capture -- a replayed graph could run beside
-// other work on the same stream's counter -- or any allocation failure).
-uint32_t *unit_sched_for(int engine, uint64_t units, uint64_t grid, int dev, hipStream_t s,
-                         int schedule = HICCL_SCHED_AUTO) {
+// Units per ticket of the dynamic schedule: one 128 KiB phased chunk; for
+// tiles enough to cover kTicketTiles tile-loads.
+uint32_t default_grab(int engine, double n) {
+  if (engine == HICCL_ENGINE_PHASE) return 1u;
+  const double g = kTicketTiles / (n + 1.0);
+  return g <= 1.0 ? 1u : (uint32_t)(g + 0.999);
+}
+
+// The counter pair for a launch of `units` work units (n inputs, packet-
+// weighted mean for a plan) on `grid` workgroups on (dev, s), or NULL for a
+// static schedule: AUTO is dynamic for the TILE engine from kDynMinInputs
+// inputs (with the static grid-stride each workgroup is bound to the same
+// addresses mod grid x 16 KiB, i.e. to a fixed subset of DRAM channels, and
+// the ones on slow channels straggle: 5.6-5.7 vs 6.3-6.7 TB/s on C2); never
+// during stream capture (a replayed graph could run beside other work on
+// the same stream's counter); NULL also on any allocation failure.
+uint32_t *unit_sched_for(int engine, double n, uint64_t units, uint64_t grid, int dev, hipStream_t s,
+                         int schedule = HICCL_SCHED_AUTO, uint32_t grab = 0) {
   if (schedule == HICCL_SCHED_STATIC) return nullptr;
-  if (schedule == HICCL_SCHED_AUTO && engine != HICCL_ENGINE_PHASE) return nullptr;
-  if (units < kDynMinUnitsPerWG * grid) return nullptr;
+  if (schedule == HICCL_SCHED_AUTO && (engine != HICCL_ENGINE_TILE || n < kDynMinInputs)) return nullptr;
+  if (!grab) grab = default_grab(engine, n);
+  if ((units + grab - 1) / grab < kDynMinUnitsPerWG * grid) return nullptr;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
   std::lock_guard<std::mutex> lk(g_sched_mu);
@@ -789,11 +826,10 @@ constexpr int kDefUnroll = 4;
 constexpr int kDefPol = 11;  // nt loads, nt stores
 constexpr int kDefBpc = 1;
 constexpr int kPhBlock = 512;
-// auto engine: phased when the work gives every CU at least this many chunks
-// and the computes sum at least kPhaseMinInputs inputs (on fewer streams the
-// tile order is as fast: profiles/r01_crossover.jsonl)
+// auto engine: with >= 5 inputs the TILE engine on the dynamic schedule;
+// with fewer, PHASE (static) when every CU gets a chunk, else TILE
+// (profiles/r01_schedsweep*.jsonl, r01_crossover.jsonl).
 constexpr uint64_t kPhaseMinChunksPerCU = 1;
-constexpr uint32_t kPhaseMinInputs = 5;
 
 // P of the phased engine: 16 packets per lane (acc + two in-flight loads =
 // 3 x 64 VGPRs at 512 lanes) unless the accumulator is wider than a packet
@@ -810,12 +846,12 @@ int phase_p_dtype(int dtype, int acc) {
 }
 
 struct Cfg {
-  int block, unroll, bpc, nt, acc, grid, store, engine, schedule;
+  int block, unroll, bpc, nt, acc, grid, store, engine, schedule, grab, drain;
 };
 
 // Raw config: zero block/unroll stay zero until the engine is known.
 Cfg resolve(const hiccl_reduce_config_t *c) {
-  Cfg r{0, 0, kDefBpc, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO, HICCL_SCHED_AUTO};
+  Cfg r{0, 0, kDefBpc, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO, HICCL_SCHED_AUTO, 0, 0};
   if (c) {
     r.block = c->block;
     r.unroll = c->unroll;
@@ -826,6 +862,8 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
     if (c->store_policy) r.store = c->store_policy - 1;
     r.engine = c->engine;
     r.schedule = c->schedule;
+    r.grab = c->grab;
+    r.drain = c->drain;
   }
   return r;
 }
@@ -833,10 +871,12 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
 // Auto engine from the packets per input of a launch (summed over its
 // computes) and the number of inputs (packet-weighted mean for a plan).
 int auto_engine(uint64_t npkt, double n, int dtype, int acc, int dev) {
+  // bf16: the phased engine stays ahead at every size with a chunk per CU
+  // (C4 bf16 64 MiB: 5.9-6.1 vs 5.0 TB/s tile; 1-4 GiB: on par)
+  if (n >= kDynMinInputs && dtype != HICCL_BFLOAT16) return HICCL_ENGINE_TILE;
   const uint64_t chunk = (uint64_t)kPhBlock * phase_p_dtype(dtype, acc);
-  return (n >= kPhaseMinInputs && npkt >= kPhaseMinChunksPerCU * (uint64_t)device_cus(dev) * chunk)
-             ? HICCL_ENGINE_PHASE
-             : HICCL_ENGINE_TILE;
+  return npkt >= kPhaseMinChunksPerCU * (uint64_t)device_cus(dev) * chunk ? HICCL_ENGINE_PHASE
+                                                                          : HICCL_ENGINE_TILE;
 }
 
 // Fill in the engine and its default shape.
@@ -956,16 +996,16 @@ uint64_t unit_pkts(int engine, int dtype, int acc) {
                                       : (uint64_t)kPlanBlock * kPlanUnroll;
 }
 
-typedef void (*plan_fn)(const PlanDesc *, uint32_t, uint32_t, uint64_t, uint64_t, uint32_t *, dim3,
-                        hipStream_t);
+typedef void (*plan_fn)(const PlanDesc *, uint32_t, uint32_t, uint64_t, uint64_t, uint32_t *, uint32_t,
+                        dim3, hipStream_t);
 
 template <class Op, int ENG>
 void launch_plan_t(const PlanDesc *d, uint32_t c0, uint32_t ncomp, uint64_t t0, uint64_t t1,
-                   uint32_t *sched, dim3 grid, hipStream_t s) {
+                   uint32_t *sched, uint32_t grab, dim3 grid, hipStream_t s) {
   constexpr int B = ENG == kPhase ? kPhBlock : kPlanBlock;
   constexpr int U = ENG == kPhase ? phase_p<Op>() : kPlanUnroll;
   hipLaunchKernelGGL((k_reduce_plan<Op, B, U, kDefPol, ENG>), grid, dim3(B), 0, s, d, c0, ncomp, t0, t1,
-                     sched);
+                     sched, grab);
 }
 
 template <class Op>
@@ -1024,6 +1064,7 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
     return fail(hipErrorInvalidValue, "hiccl_reduce: bad engine");
   if (c.schedule < HICCL_SCHED_AUTO || c.schedule > HICCL_SCHED_DYNAMIC)
     return fail(hipErrorInvalidValue, "hiccl_reduce: bad schedule");
+  if (c.grab < 0 || c.grab > 4096) return fail(hipErrorInvalidValue, "hiccl_reduce: bad grab");
   hipStream_t s = (hipStream_t)stream;
   const int dev = current_device();
   Split sp = split_on(out, count, esz);
@@ -1054,7 +1095,9 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
 
   uint64_t grid = c.grid > 0 ? (uint64_t)c.grid : (uint64_t)device_cus(dev) * c.bpc;
   if (grid > a.ntiles) grid = a.ntiles;
-  a.sched = unit_sched_for(c.engine, a.ntiles, grid, dev, s, c.schedule);
+  a.grab = c.grab > 0 ? (uint32_t)c.grab : default_grab(c.engine, n);
+  a.drain = (uint32_t)c.drain;
+  a.sched = unit_sched_for(c.engine, n, a.ntiles, grid, dev, s, c.schedule, a.grab);
   fn(a, dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "hiccl_reduce: launch");
 }
@@ -1082,6 +1125,7 @@ struct hiccl_reduce_plan {
   int acc = HICCL_ACC_NATIVE;
   int engine_req = HICCL_ENGINE_AUTO;  // hiccl_reduce_plan_set_engine
   int engine = HICCL_ENGINE_TILE;      // resolved at upload
+  double mean_n = 0;                   // packet-weighted inputs per compute
   size_t esz = 0;
   struct Comp {
     void *out;
@@ -1127,6 +1171,7 @@ int plan_upload(hiccl_reduce_plan *p) {
     weighted_n += (double)k * c.in.size();
   }
   const double mean_n = total_pkt ? weighted_n / total_pkt : 0;
+  p->mean_n = mean_n;
   p->engine = p->engine_req != HICCL_ENGINE_AUTO
                   ? p->engine_req
                   : auto_engine(total_pkt, mean_n, p->dtype, p->acc, p->device);
@@ -1167,7 +1212,8 @@ int plan_kernel(hiccl_reduce_plan *p, uint32_t c0, uint64_t t0, uint64_t t1, int
   uint64_t grid = (uint64_t)device_cus(p->device) * kPlanBpc;
   if (grid > t1 - t0) grid = t1 - t0;
   fn(p->d_desc, c0, (uint32_t)p->comps.size(), t0, t1,
-     unit_sched_for(p->engine, t1 - t0, grid, p->device, s), dim3((unsigned)grid), s);
+     unit_sched_for(p->engine, p->mean_n, t1 - t0, grid, p->device, s), default_grab(p->engine, p->mean_n),
+     dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "plan: launch");
 }
 
@@ -1198,8 +1244,8 @@ int reduce_via_table(int dtype, int acc, int engine, void *out, const void *cons
   plan_fn fn = pick_plan(dtype, acc, engine);
   uint64_t grid = (uint64_t)device_cus(current_device()) * kPlanBpc;
   if (grid > tiles) grid = tiles;
-  fn((const PlanDesc *)dmem, 0, 1, 0, tiles, unit_sched_for(engine, tiles, grid, current_device(), s),
-     dim3((unsigned)grid), s);
+  fn((const PlanDesc *)dmem, 0, 1, 0, tiles, unit_sched_for(engine, n, tiles, grid, current_device(), s),
+     default_grab(engine, n), dim3((unsigned)grid), s);
   if (int e = check_hip(hipGetLastError(), "hiccl_reduce: launch")) return e;
   return check_hip(hipFreeAsync(dmem, s), "hiccl_reduce: hipFreeAsync");
 }

@@ -50,15 +50,14 @@ typedef enum {
 } hiccl_acc_t;
 
 /* Kernel engine (both compute the same bits; they differ in access order).
- *   TILE   all n inputs of a 16 KiB-per-input tile are loaded together;
- *          suits computes too small to give every CU several chunks.
+ *   TILE   all n inputs of a 16 KiB-per-input tile are loaded together.
  *   PHASE  a workgroup sweeps a 128 KiB chunk of input 0, then of input 1,
  *          ... (next input's loads in flight while the current one is
- *          added), then writes the chunk: only ~2 input streams are open
- *          chip-wide at a time.  Default for large buckets.
- *   AUTO   PHASE when there are >= 5 inputs and every CU gets >= 1 chunk
+ *          added), then writes the chunk.
+ *   AUTO   TILE (on the dynamic schedule, below) with >= 5 inputs, except
+ *          bf16; otherwise PHASE when every CU gets >= 1 chunk, else TILE
  *          (one-shot: that call; plan: all computes, packet-weighted mean
- *          n), else TILE. */
+ *          n). */
 typedef enum {
   HICCL_ENGINE_AUTO = 0,
   HICCL_ENGINE_TILE = 1,
@@ -67,11 +66,13 @@ typedef enum {
 
 /* Work-unit schedule (same bits either way).
  *   STATIC   workgroup b takes units b, b + grid, ...
- *   DYNAMIC  workgroups take their next unit from a device counter (one per
- *            device and stream, reset by the launch itself): faster-served
- *            workgroups do more units, the tail is one unit.
- *   AUTO     DYNAMIC for the PHASE engine with >= 4 units per workgroup,
- *            STATIC otherwise and always during stream capture.
+ *   DYNAMIC  workgroups take their next `grab` units from a device counter
+ *            (one per device and stream, reset by the launch itself):
+ *            faster-served workgroups do more units, the tail is one ticket.
+ *   AUTO     DYNAMIC for the TILE engine with >= 5 inputs and >= 32 tickets
+ *            per workgroup, STATIC otherwise and always during stream
+ *            capture.  A forced DYNAMIC still needs >= 32 tickets per
+ *            workgroup. 
  * Plans use AUTO. */
 typedef enum {
   HICCL_SCHED_AUTO = 0,
@@ -122,6 +123,9 @@ typedef struct {
   int store_policy;  /* stores: 1 plain, 2 nt, 3 sc1 (write-through, line dropped from L2) */
   int engine;        /* hiccl_engine_t */
   int schedule;      /* hiccl_schedule_t */
+  int grab;          /* dynamic schedule: units per ticket (0 = default: PHASE 1,
+                        TILE ceil(9 / (n + 1))) */
+  int drain;         /* 1: a workgroup waits for a unit's stores before the next unit's loads */
 } hiccl_reduce_config_t;
 
 int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t count,

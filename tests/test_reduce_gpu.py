@@ -156,21 +156,22 @@ def test_phase_variants_same_bits(oracle, config):
 
 
 @pytest.mark.parametrize("engine", [1, 2], ids=["tile", "phase"])
-@pytest.mark.parametrize("grid", [4, 16])
+@pytest.mark.parametrize("grid", [1, 2])
 def test_dynamic_schedule_same_bits(oracle, engine, grid):
     """Dynamic unit scheduling (device ticket counter, reset by the launch
     itself) against static, repeated launches on one stream (the counter
     must come back to zero each time: a stale counter would skip units and
     leave the NaN prefill), and a second stream (its own counter)."""
     S = hiccl_amd._lib
-    for n, count in ((8, (1 << 20) + 5), (3, 777777)):
+    # >= 32 tickets per workgroup (the dynamic threshold): 64+ phased chunks
+    for n, count in ((8, (1 << 21) + 5), (3, (1 << 21) + 33333)):
         x = oracle.fill(n, count, seed=n + grid)
         exp = oracle.reduce(list(x))
         ins = [to_dev(r) for r in x]
         out = torch.empty(count, device=DEV)
         side = torch.cuda.Stream()
         for sched in (S.HICCL_SCHED_STATIC, S.HICCL_SCHED_DYNAMIC):
-            cfg = dict(engine=engine, grid=grid, schedule=sched)
+            cfg = dict(engine=engine, grid=grid, schedule=sched, grab=1)
             for rep in range(5):
                 out.fill_(float("nan"))
                 hiccl_amd.reduce(out, ins, config=cfg)
@@ -187,14 +188,15 @@ def test_dynamic_schedule_same_bits(oracle, engine, grid):
 
 
 def test_dynamic_schedule_plan_many_computes(oracle):
-    """A phased plan big enough for the dynamic schedule (>= 4 units per
-    workgroup), many computes of ragged sizes, launched 3 times."""
+    """An AUTO plan big enough for the dynamic schedule (tile engine, mean n
+    >= 5, >= 32 tickets per workgroup of 256), many computes of ragged
+    sizes, launched 3 times."""
     rng = np.random.default_rng(11)
-    comp = hiccl_amd.Compute(torch.float32, device=0, engine=hiccl_amd.HICCL_ENGINE_PHASE)
+    comp = hiccl_amd.Compute(torch.float32, device=0)
     outs, exps, keep = [], [], []
     for c in range(300):
-        n = int(rng.integers(1, 9))
-        count = int(rng.integers(1, 400000))  # ~2,000 units of 128 KiB: dynamic
+        n = int(rng.integers(5, 10))
+        count = int(rng.integers(1, 600000))  # ~11,000 two-tile tickets
         x = oracle.fill(n, count, seed=500 + c)
         ins = [to_dev(r) for r in x]
         keep += ins
@@ -343,15 +345,15 @@ def test_plan_phase_engine(oracle, each):
 
 
 def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
-    """AUTO resolves to PHASE with >= 5 inputs once every CU gets a chunk
-    of 128 KiB (f32: 2^23 elements per input on 256 CUs), to TILE below or
-    with fewer inputs."""
+    """AUTO resolves to TILE with >= 5 inputs; with fewer, to PHASE once
+    every CU gets a chunk of 128 KiB (f32: 2^23 elements per input on 256
+    CUs), to TILE below."""
     count = 1 << 23
     a = torch.empty(count, device=DEV)
     hiccl_amd.fill_uniform(a, 77, 0)
     out = torch.empty(count, device=DEV)
     P, T = hiccl_amd.HICCL_ENGINE_PHASE, hiccl_amd.HICCL_ENGINE_TILE
-    for cnt, n, expect in ((count, 6, P), (count, 2, T), (count // 4, 6, T)):
+    for cnt, n, expect in ((count, 6, T), (count, 2, P), (count // 4, 6, T), (count // 4, 2, T)):
         comp = hiccl_amd.Compute(torch.float32, device=0)
         comp.add([a] * n, out, cnt, compid=0)
         comp.start()
