@@ -12,8 +12,12 @@
 //  * 16-byte packets per lane (global_load_dwordx4 with an SGPR base +
 //    32-bit lane offset), U packets per input per lane per tile, so each
 //    lane has G*U independent 16-B loads in flight before the in-order adds;
-//  * a persistent grid (CUs x blocks_per_cu workgroups) sweeping tiles
-//    grid-stride, full tiles unpredicated;
+//  * a persistent grid (CUs x blocks_per_cu workgroups); work units handed
+//    out grid-stride or by a device ticket counter (dynamic schedule: no
+//    workgroup is bound to a fixed subset of DRAM channels), buffer
+//    descriptors make partial units predicate-free;
+//  * two engines: TILE (all n inputs of a 16 KiB tile loaded together) and
+//    PHASE (a 128 KiB chunk swept input by input); AUTO picks per launch;
 //  * the input pointer table travels in the kernarg segment (scalar loads,
 //    no device-side T** table and no H2D copy per call, cf. compute.h:124-126);
 //  * the output is 16-B aligned by peeling a scalar head; inputs may be
