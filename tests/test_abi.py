@@ -68,10 +68,12 @@ def test_invalid_arguments_rejected_on_host():
     # unsupported tuning config
     cfg = L.ReduceConfig(block=128)
     assert lib.hiccl_reduce_ex(0, ctypes.c_void_p(0x1000), _tab([0x2000]), 1, 4, None, ctypes.byref(cfg)) == 1
-    # unknown engine
-    cfg = L.ReduceConfig(engine=7)
-    assert lib.hiccl_reduce_ex(0, ctypes.c_void_p(0x1000), _tab([0x2000]), 1, 4, None, ctypes.byref(cfg)) == 1
-    assert "engine" in L.last_error()
+    # unknown engine / schedule, bad grab
+    for bad, word in ((dict(engine=7), "engine"), (dict(schedule=5), "schedule"), (dict(grab=-1), "grab"),
+                      (dict(grab=100000), "grab")):
+        cfg = L.ReduceConfig(**bad)
+        assert lib.hiccl_reduce_ex(0, ctypes.c_void_p(0x1000), _tab([0x2000]), 1, 4, None, ctypes.byref(cfg)) == 1
+        assert word in L.last_error()
     # plan NULL handling
     assert lib.hiccl_reduce_plan_launch(None, None) == 1
     assert lib.hiccl_reduce_plan_set_engine(None, L.HICCL_ENGINE_PHASE) == 1

@@ -215,6 +215,41 @@ def test_dynamic_schedule_plan_many_computes(oracle):
     comp.close()
 
 
+@pytest.mark.parametrize("eng", [None, PHASE], ids=["auto", "phase"])
+def test_graph_capture_replay(oracle, eng):
+    """hiccl_reduce captured into a HIP graph (torch.cuda.graph) and
+    replayed with new input values: during capture the library takes the
+    static schedule (a replayed graph must not share a stream's ticket
+    counter), and every replay gives the reference bits."""
+    n, count = 8, (1 << 24) + 3  # big enough that AUTO would go dynamic uncaptured
+    ins = [torch.empty(count, device=DEV) for _ in range(n)]
+    out = torch.empty(count, device=DEV)
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, 1, k)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        hiccl_amd.reduce(out, ins, config=eng)  # warm-up outside capture
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        hiccl_amd.reduce(out, ins, config=eng)
+    rng = np.random.default_rng(5)
+    for seed in (11, 12, 13):
+        for k, t in enumerate(ins):
+            hiccl_amd.fill_uniform(t, seed, k)
+        out.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        idx = np.concatenate([np.arange(16), count - 16 + np.arange(16),
+                              rng.integers(0, count, 2048)]).astype(np.int64)
+        got = out[torch.from_numpy(idx).to(DEV)].cpu().numpy()
+        exp = oracle.sample_sum(idx.astype(np.uint64), seed, n)
+        assert bits_equal(got, exp), (seed, first_mismatch(got, exp))
+
+
 def test_phase_unsupported_shape_is_an_error():
     x = torch.zeros(100, device=DEV)
     with pytest.raises(hiccl_amd.HicclError):
