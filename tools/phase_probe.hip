@@ -610,6 +610,188 @@ static int launch_dyn(int grid, const PArgs &a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Per-WAVE dynamic tiles (N = 8): every wave takes its own unit of 64 lanes
+// x U packets (U*1 KiB per input) from the ticket counter -- no workgroup
+// barrier, and the chip-wide window is 4x narrower than per-workgroup 16 KiB
+// tiles.  Next ticket grabbed before the current unit's loads.
+template <int B, int U>
+__global__ __launch_bounds__(B) void k_wave_dyn(PArgs a, unsigned int *counter) {
+  constexpr int N = 8;
+  constexpr uint64_t UB = 64ull * U * 16;  // bytes per input per unit
+  const uint64_t nunits = (a.bytes + UB - 1) / UB;
+  const int lane = threadIdx.x & 63;
+  uint32_t voff[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * 64 + lane) * 16);
+  uint32_t t;
+  {
+    uint32_t v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __builtin_amdgcn_readfirstlane(v);
+  }
+  while (t < nunits) {
+    uint32_t nv;
+    if (lane == 0) nv = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t off = (uint64_t)t * UB;
+    const uint32_t nb = (uint32_t)((a.bytes - off) < UB ? (a.bytes - off) : UB);
+    f32x4 x[N][U];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      rsrc_t r = mk(a.in[j] + off, nb);
+#pragma unroll
+      for (int u = 0; u < U; u++) x[j][u] = ld<2>(r, voff[u]);
+    }
+    f32x4 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) acc[u] = (f32x4)(0.0f);
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+      for (int u = 0; u < U; u++) acc[u] += x[j][u];
+    t = __builtin_amdgcn_readfirstlane(nv);
+    rsrc_t w = mk(a.out + off, nb);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[u]), w, (int)voff[u], 0, 2);
+  }
+}
+
+template <int B, int U>
+static int launch_wave_dyn(int grid, const PArgs &a, hipStream_t s) {
+  unsigned int *ctr = sync_counter();
+  if (hipMemsetAsync(ctr, 0, sizeof(unsigned int), s)) return -5;
+  hipLaunchKernelGGL((k_wave_dyn<B, U>), dim3(grid), dim3(B), 0, s, a, ctr);
+  return (int)hipGetLastError();
+}
+
+// Per-workgroup dynamic 16 KiB tiles (the product's default) for comparison
+template <int B, int U>
+__global__ __launch_bounds__(B) void k_wg_dyn(PArgs a, unsigned int *counter) {
+  constexpr int N = 8;
+  constexpr uint64_t UB = (uint64_t)B * U * 16;
+  const uint64_t nunits = (a.bytes + UB - 1) / UB;
+  uint32_t voff[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * B + threadIdx.x) * 16);
+  __shared__ uint32_t s_t[2];
+  if (threadIdx.x == 0) s_t[0] = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  uint32_t t = s_t[0];
+  int slot = 1;
+  while (t < nunits) {
+    uint32_t nv;
+    if (threadIdx.x == 0) nv = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t off = (uint64_t)t * UB;
+    const uint32_t nb = (uint32_t)((a.bytes - off) < UB ? (a.bytes - off) : UB);
+    f32x4 x[N][U];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      rsrc_t r = mk(a.in[j] + off, nb);
+#pragma unroll
+      for (int u = 0; u < U; u++) x[j][u] = ld<2>(r, voff[u]);
+    }
+    f32x4 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) acc[u] = (f32x4)(0.0f);
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+      for (int u = 0; u < U; u++) acc[u] += x[j][u];
+    if (threadIdx.x == 0) s_t[slot] = nv;
+    rsrc_t w = mk(a.out + off, nb);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[u]), w, (int)voff[u], 0, 2);
+    __syncthreads();
+    t = s_t[slot];
+    slot ^= 1;
+  }
+}
+
+template <int B, int U>
+static int launch_wg_dyn(int grid, const PArgs &a, hipStream_t s) {
+  unsigned int *ctr = sync_counter();
+  if (hipMemsetAsync(ctr, 0, sizeof(unsigned int), s)) return -5;
+  hipLaunchKernelGGL((k_wg_dyn<B, U>), dim3(grid), dim3(B), 0, s, a, ctr);
+  return (int)hipGetLastError();
+}
+
+// Dynamic tiles with C counters (64 B apart): workgroup b (wave w for
+// PER_WAVE) uses counter (b % C); its ticket k from that counter is unit
+// k*C + (b % C).  Spreads the atomic traffic over C addresses.
+template <int B, int U, int C, bool PER_WAVE>
+__global__ __launch_bounds__(B) void k_multi_dyn(PArgs a, unsigned int *counter) {
+  constexpr int N = 8;
+  constexpr int LANES = PER_WAVE ? 64 : B;
+  constexpr uint64_t UB = (uint64_t)LANES * U * 16;
+  const uint64_t nunits = (a.bytes + UB - 1) / UB;
+  const int lid = PER_WAVE ? (threadIdx.x & 63) : threadIdx.x;
+  const uint32_t who = PER_WAVE ? (blockIdx.x * (B / 64) + threadIdx.x / 64) : blockIdx.x;
+  const uint32_t cidx = who % C;
+  unsigned int *ctr = counter + cidx * 16;
+  uint32_t voff[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * LANES + lid) * 16);
+  __shared__ uint32_t s_t[2];
+  auto grab = [&]() -> uint32_t {
+    return __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  uint64_t t;
+  if (PER_WAVE) {
+    uint32_t v = 0;
+    if (lid == 0) v = grab();
+    t = (uint64_t)__builtin_amdgcn_readfirstlane(v) * C + cidx;
+  } else {
+    if (threadIdx.x == 0) s_t[0] = grab();
+    __syncthreads();
+    t = (uint64_t)s_t[0] * C + cidx;
+  }
+  int slot = 1;
+  while (t < nunits) {
+    uint32_t nv;
+    if (lid == 0) nv = grab();
+    const uint64_t off = t * UB;
+    const uint32_t nb = (uint32_t)((a.bytes - off) < UB ? (a.bytes - off) : UB);
+    f32x4 x[N][U];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      rsrc_t r = mk(a.in[j] + off, nb);
+#pragma unroll
+      for (int u = 0; u < U; u++) x[j][u] = ld<2>(r, voff[u]);
+    }
+    f32x4 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) acc[u] = (f32x4)(0.0f);
+#pragma unroll
+    for (int j = 0; j < N; j++)
+#pragma unroll
+      for (int u = 0; u < U; u++) acc[u] += x[j][u];
+    if (PER_WAVE) {
+      t = (uint64_t)__builtin_amdgcn_readfirstlane(nv) * C + cidx;
+    } else if (threadIdx.x == 0) {
+      s_t[slot] = nv;
+    }
+    rsrc_t w = mk(a.out + off, nb);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[u]), w, (int)voff[u], 0, 2);
+    if (!PER_WAVE) {
+      __syncthreads();
+      t = (uint64_t)s_t[slot] * C + cidx;
+      slot ^= 1;
+    }
+  }
+}
+
+template <int B, int U, int C, bool PW>
+static int launch_multi_dyn(int grid, const PArgs &a, hipStream_t s) {
+  static_assert(C * 16 <= 64, "counters are 16 words apart; only 64 words are cleared");
+  unsigned int *ctr = sync_counter();
+  if (hipMemsetAsync(ctr, 0, 64 * sizeof(unsigned int), s)) return -5;
+  hipLaunchKernelGGL((k_multi_dyn<B, U, C, PW>), dim3(grid), dim3(B), 0, s, a, ctr);
+  return (int)hipGetLastError();
+}
+
 // Product tile order (all n inputs of a tile loaded together), slab-walked.
 template <int B, int U, int AUXL, int AUXS>
 __global__ __launch_bounds__(B) void k_slab(PArgs a) {
@@ -715,6 +897,24 @@ int pp_run(int kind, int block, int param, int depth, int nt, int grid, const vo
     if (block == 512 && param == 16) return launch_dyn<512, 16>(grid, a, s);
     if (block == 1024 && param == 8) return launch_dyn<1024, 8>(grid, a, s);
     if (block == 512 && param == 8) return launch_dyn<512, 8>(grid, a, s);
+  } else if (kind == 10) {  // per-wave dynamic, param = U
+    if (n != 8) return -3;
+    if (block == 256 && param == 4) return launch_wave_dyn<256, 4>(grid, a, s);
+    if (block == 512 && param == 4) return launch_wave_dyn<512, 4>(grid, a, s);
+    if (block == 256 && param == 2) return launch_wave_dyn<256, 2>(grid, a, s);
+    if (block == 1024 && param == 4) return launch_wave_dyn<1024, 4>(grid, a, s);
+  } else if (kind == 11) {  // per-workgroup dynamic tiles
+    if (n != 8) return -3;
+    if (block == 256 && param == 4) return launch_wg_dyn<256, 4>(grid, a, s);
+    if (block == 256 && param == 2) return launch_wg_dyn<256, 2>(grid, a, s);
+    if (block == 512 && param == 2) return launch_wg_dyn<512, 2>(grid, a, s);
+  } else if (kind == 12) {  // multi-counter dynamic: depth = C; nt = 1 per-wave
+    if (n != 8) return -3;
+    if (block == 256 && param == 4 && depth == 2 && !nt) return launch_multi_dyn<256, 4, 2, false>(grid, a, s);
+    if (block == 256 && param == 4 && depth == 4 && !nt) return launch_multi_dyn<256, 4, 4, false>(grid, a, s);
+    if (block == 256 && param == 2 && depth == 4 && !nt) return launch_multi_dyn<256, 2, 4, false>(grid, a, s);
+    if (block == 256 && param == 4 && depth == 4 && nt) return launch_multi_dyn<256, 4, 4, true>(grid, a, s);
+    if (block == 256 && param == 4 && depth == 2 && nt) return launch_multi_dyn<256, 4, 2, true>(grid, a, s);
   } else if (kind == 4) {  // depth = MODE
     if (n != 8) return -3;
     if (block == 512 && param == 16 && depth == 0) return launch(k_phase_x<512, 16, 0>, grid, 512, a, s);

@@ -65,9 +65,10 @@ def main():
     modes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2").split(",")]
     buckets = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     # (kind, block, param, depth, nt, grid); kind 0 phase (runtime n), 1 slab, 2 phase_n (n = 8)
-    variants = [(2, 512, 16, 2, 1, 256), (9, 512, 16, 0, 1, 256), (9, 1024, 8, 0, 1, 256),
-                (9, 512, 8, 0, 1, 256), (9, 512, 8, 0, 1, 512), (9, 512, 16, 0, 1, 256),
-                (2, 512, 16, 2, 1, 256)]
+    # kind 12: (12, block, U, C, per_wave, grid)
+    variants = [(11, 256, 4, 0, 1, 256), (12, 256, 4, 2, 0, 256), (12, 256, 4, 4, 0, 256),
+                (12, 256, 4, 8, 0, 256), (12, 256, 2, 4, 0, 256), (12, 256, 2, 8, 0, 256),
+                (12, 256, 4, 4, 1, 256), (12, 256, 4, 2, 1, 256), (11, 256, 4, 0, 1, 256)]
     g = P.pp_granularity()
     print(json.dumps({"vmm_granularity_min": g >> 32, "vmm_granularity_rec": g & 0xffffffff}), flush=True)
     stream = torch.cuda.current_stream()
@@ -100,7 +101,7 @@ def main():
                 torch.cuda.synchronize()
                 diff = P.pp_diff(vp(out), vp(ref), NB) if not (kind == 4 and depth < 16 and depth & 1) else None
                 print(json.dumps({"alloc": mode, "bucket": b,
-                                  "kernel": ["phase", "slab", "phase_n", "phase_lds", "phase_x", "phase_flat", "phase_pipe", "phase_sync", "phase_q", "phase_dyn"][kind], "block": block,
+                                  "kernel": ["phase", "slab", "phase_n", "phase_lds", "phase_x", "phase_flat", "phase_pipe", "phase_sync", "phase_q", "phase_dyn", "wave_dyn", "wg_dyn", "multi_dyn"][kind], "block": block,
                                   "param": param, "depth": depth, "nt": nt, "grid": grid, "ms": round(ms, 4),
                                   "GBps": round(9 * NB / ms / 1e6, 1), "mismatch_words": diff}), flush=True)
             if H is not None:
