@@ -319,6 +319,9 @@ def main():
     ap.add_argument("--crossover", action="store_true")
     ap.add_argument("--planvs", action="store_true")
     ap.add_argument("--schedsweep", action="store_true")
+    ap.add_argument("--xdtype", default="both", help="crossover: f32 | bf16 | both")
+    ap.add_argument("--xmib", default="", help="crossover: comma list of MiB per input")
+    ap.add_argument("--xn", default="", help="crossover: comma list of input counts")
     ap.add_argument("--buckets", type=int, default=0, help="schedsweep: this many fresh --n x 2^--log2count buckets")
     args = ap.parse_args()
 
@@ -564,10 +567,14 @@ def planvs(args):
 def crossover(args):
     """Engine crossover: one-shot reduce of n = 2/4/8 inputs, 1-512 MiB per
     input, f32 and bf16, TILE vs PHASE (sets the AUTO threshold)."""
-    for dtype in (torch.float32, torch.bfloat16):
+    dtypes = {"f32": (torch.float32,), "bf16": (torch.bfloat16,)}.get(args.xdtype,
+                                                                     (torch.float32, torch.bfloat16))
+    mibs = [int(m) for m in args.xmib.split(",")] if args.xmib else (1, 4, 16, 32, 64, 128, 256, 512)
+    ns = [int(m) for m in args.xn.split(",")] if args.xn else (2, 4, 8)
+    for dtype in dtypes:
         esz = torch.tensor([], dtype=dtype).element_size()
-        for n in (2, 4, 8):
-            for mib in (1, 4, 16, 32, 64, 128, 256, 512):
+        for n in ns:
+            for mib in mibs:
                 count = (mib << 20) // esz
                 ins, out = make_bucket(n, count, dtype)
                 row = {"mode": "crossover", "dtype": str(dtype).split(".")[-1], "n": n, "mib_per_input": mib}
@@ -626,7 +633,7 @@ def chunks(args):
                 continue
             ins, out = make_bucket(n, count, dtype)
             depth = max(1, (mib << 20) // (1 << 20))
-            comp = hiccl_amd.Compute(dtype, device=torch.cuda.current_device())
+            comp = hiccl_amd.Compute(dtype, device=torch.cuda.current_device(), engine=args.engine)
             off = 0
             for b in range(depth):  # partition(): count/numbatch + (b < count%numbatch)
                 c = count // depth + (1 if b < count % depth else 0)
@@ -642,7 +649,7 @@ def chunks(args):
             b = (n + 1) * count * esz
             ok = sample_check(out, n, count, bf16=(dtype == torch.bfloat16))
             print(json.dumps({"config": "C4", "dtype": str(dtype).split(".")[-1], "mib_per_input": mib,
-                              "parity_sample_ok": ok,
+                              "parity_sample_ok": ok, "engine": comp.engine(),
                               "computes": depth, "batched_ms": round(res["batched"] * 1e3, 4),
                               "batched_GBps": round(b / res["batched"] / 1e9, 1),
                               "each_ms": round(res["each"] * 1e3, 4),
@@ -651,6 +658,15 @@ def chunks(args):
             del ins, out
             torch.cuda.empty_cache()
     return 0
+
+
+def host_sum(host_in):
+    """In-order fp32 sum on the host (torch adds two tensors element-wise in
+    fp32 with round-to-nearest: the reference's acc += in[k][i] order)."""
+    exp = torch.zeros_like(host_in[0])
+    for h in host_in:
+        exp = exp + h
+    return exp
 
 
 def roundtrip(args):
@@ -690,18 +706,27 @@ def roundtrip(args):
         for s in streams:
             cur.wait_stream(s)
 
+    pipes = {f"host_pipe_{mib}MiB_d{d}": hiccl_amd.HostPipe(torch.float32, chunk_bytes=mib << 20, depth=d)
+             for mib, d in ((64, 3), (32, 4), (128, 2))}
+    legs = [("serial", serial), ("pipelined", pipelined)]
+    expect = host_sum(host_in)
+    legs += [(k, (lambda p=p: p.reduce(host_out, host_in))) for k, p in pipes.items()]
     out = {}
-    for name, fn in (("serial", serial), ("pipelined", pipelined)):
+    for name, fn in legs:
+        host_out.zero_()
         wall, _ = time_launches(fn, 5, 2)
         t = wall / 5
         out[name] = {"s": round(t, 4), "GBps_alg": round((n + 1) * count * 4 / t / 1e9, 2)}
+        if name.startswith("host_pipe"):
+            out[name]["parity_ok"] = bool(torch.equal(host_out.view(torch.int32), expect.view(torch.int32)))
+    for p in pipes.values():
+        p.close()
     # device-only reference
     _, ms = time_launches(lambda: hiccl_amd.reduce(dev_out, dev_in), 10, 3)
     out["kernel_only_GBps"] = round((n + 1) * count * 4 / (np.median(ms) * 1e-3) / 1e9, 1)
-    exp = host_in[0].clone()
-    for h in host_in[1:]:
-        exp = exp + h
+    pipelined()
     torch.cuda.synchronize()
+    exp = expect
     out["parity_ok"] = bool(torch.equal(exp.view(torch.int32), host_out.view(torch.int32)))
     print(json.dumps({"mode": "roundtrip", "n": n, "count": count, **out,
                       "pcie_bytes": (n + 1) * count * 4}), flush=True)

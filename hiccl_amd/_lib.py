@@ -86,6 +86,10 @@ _SIGS = {
     "hiccl_reduce_plan_stream": (_vp, [_vp]),
     "hiccl_reduce_plan_bytes": (ctypes.c_size_t, [_vp]),
     "hiccl_reduce_plan_destroy": (None, [_vp]),
+    "hiccl_host_pipe_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_size_t, ctypes.c_int]),
+    "hiccl_host_pipe_reduce": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_size_t]),
+    "hiccl_host_pipe_destroy": (None, [_vp]),
     "hiccl_fill_uniform": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_size_t, ctypes.c_uint64,
                                           ctypes.c_uint32, ctypes.c_size_t, _vp]),
     "hiccl_stream_copy": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),

@@ -212,6 +212,53 @@ class Compute:
             pass
 
 
+class HostPipe:
+    """Host-resident buckets (include/hiccl_reduce.h hiccl_host_pipe_*):
+    ``reduce(out, inputs)`` sums host tensors in list order on the GPU,
+    staging ``chunk_bytes`` per input through device memory with H2D /
+    kernel / D2H pipelined over ``depth`` streams.  Blocking; same bits as
+    :func:`reduce`.  Pin the tensors (``pin_memory()``) for the overlap."""
+
+    def __init__(self, dtype=torch.float32, device=None, chunk_bytes=0, depth=0):
+        self.dtype = dtype
+        self.code = L.DTYPE_OF_TORCH[dtype]
+        if device is None:
+            device = torch.cuda.current_device()
+        h = ctypes.c_void_p()
+        L.check(L.lib().hiccl_host_pipe_create(ctypes.byref(h), self.code, device, chunk_bytes, depth),
+                "host_pipe_create")
+        self._pipe = h
+
+    def reduce(self, out, inputs, count=None):
+        for k, t in enumerate([out] + list(inputs)):
+            what = "out" if k == 0 else f"inputs[{k - 1}]"
+            if not isinstance(t, torch.Tensor) or t.is_cuda:
+                raise ValueError(f"hiccl: {what} must be a host tensor (HostPipe stages it to the GPU)")
+            if not t.is_contiguous():
+                raise ValueError(f"hiccl: {what} must be contiguous")
+            if t.dtype != self.dtype:
+                raise TypeError(f"hiccl: {what} dtype {t.dtype} != pipe dtype {self.dtype}")
+        if count is None:
+            count = out.numel()
+        if any(t.numel() < count for t in [out] + list(inputs)):
+            raise ValueError(f"hiccl: a buffer has fewer than count={count} elements")
+        tab = _ptr_table([t.data_ptr() for t in inputs])
+        L.check(L.lib().hiccl_host_pipe_reduce(self._pipe, ctypes.c_void_p(out.data_ptr()), tab,
+                                               len(inputs), count), "host_pipe_reduce")
+        return out
+
+    def close(self):
+        if self._pipe:
+            L.lib().hiccl_host_pipe_destroy(self._pipe)
+            self._pipe = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def fill_uniform(t, seed, k, first=0, stream=None):
     """Synthetic input k: uniform [-1,1) of hash(seed, k, first + i) (matches the oracle)."""
     _check_tensor(t, "t")

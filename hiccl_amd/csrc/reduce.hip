@@ -722,6 +722,8 @@ constexpr double kDynMinInputs = 5;
 // ((n + 1) per tile): one tile at n >= 8, two at n = 4..7, ... -- a ticket
 // costs an atomic and a workgroup barrier (profiles/r01_schedsweep*.jsonl).
 constexpr double kTicketTiles = 9;
+// bf16 takes the tile engine (AUTO) only from this many tickets per workgroup.
+constexpr uint64_t kBf16TileMinTicketsPerWG = 64;
 
 // Units per ticket of the dynamic schedule: one 128 KiB phased chunk; for
 // tiles enough to cover kTicketTiles tile-loads.
@@ -875,9 +877,16 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
 // Auto engine from the packets per input of a launch (summed over its
 // computes) and the number of inputs (packet-weighted mean for a plan).
 int auto_engine(uint64_t npkt, double n, int dtype, int acc, int dev) {
-  // bf16: the phased engine stays ahead at every size with a chunk per CU
-  // (C4 bf16 64 MiB: 5.9-6.1 vs 5.0 TB/s tile; 1-4 GiB: on par)
-  if (n >= kDynMinInputs && dtype != HICCL_BFLOAT16) return HICCL_ENGINE_TILE;
+  if (n >= kDynMinInputs) {
+    if (dtype != HICCL_BFLOAT16) return HICCL_ENGINE_TILE;
+    // bf16 (packed accumulator) adds 3x the VALU work per tile: the tile
+    // engine needs more tickets per workgroup before it passes the phased
+    // one (n = 8: 128 MiB per input 6.00 vs 6.28, 256 MiB 6.38 vs 6.23,
+    // 1 GiB 6.50 vs 6.09 TB/s; profiles/r01g_bf16_crossover.jsonl)
+    const uint64_t tickets = npkt / ((uint64_t)kDefBlock * kDefUnroll) / default_grab(HICCL_ENGINE_TILE, n);
+    if (acc == HICCL_ACC_NATIVE && tickets >= kBf16TileMinTicketsPerWG * (uint64_t)device_cus(dev))
+      return HICCL_ENGINE_TILE;
+  }
   const uint64_t chunk = (uint64_t)kPhBlock * phase_p_dtype(dtype, acc);
   return npkt >= kPhaseMinChunksPerCU * (uint64_t)device_cus(dev) * chunk ? HICCL_ENGINE_PHASE
                                                                           : HICCL_ENGINE_TILE;
@@ -1376,6 +1385,120 @@ void hiccl_reduce_plan_destroy(hiccl_reduce_plan_t *p) {
   if (p->d_ptrs) (void)hipFree(p->d_ptrs);
   if (p->done) (void)hipEventDestroy(p->done);
   if (p->own) (void)hipStreamDestroy(p->own);
+  delete p;
+}
+
+// -------------------------------------------------- host-resident buckets --
+
+}  // extern "C"
+
+struct hiccl_host_pipe {
+  int dtype = 0;
+  int device = 0;
+  size_t esz = 0;
+  size_t chunk = 0;  // elements per input per chunk
+  int depth = 0;
+  int cap_n = 0;     // staging slots hold this many inputs
+  std::vector<hipStream_t> streams;
+  std::vector<char *> stage;  // per slot: max(cap_n, 1) x chunk elements
+};
+
+namespace {
+
+constexpr size_t kPipeChunkBytes = 64ull << 20;
+constexpr int kPipeDepth = 3;
+
+int pipe_stage_for(hiccl_host_pipe *p, int n) {
+  const int need = n > 0 ? n : 1;
+  if (need <= p->cap_n) return 0;
+  for (auto &b : p->stage)
+    if (b) { (void)hipFree(b); b = nullptr; }
+  p->cap_n = 0;
+  for (auto &b : p->stage)
+    if (int e = check_hip(hipMalloc((void **)&b, (size_t)need * p->chunk * p->esz), "host_pipe: hipMalloc staging"))
+      return e;
+  p->cap_n = need;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hiccl_host_pipe_create(hiccl_host_pipe_t **pipe, int dtype, int device, size_t chunk_bytes,
+                           int depth) {
+  if (!pipe) return fail(hipErrorInvalidValue, "host_pipe_create: pipe is NULL");
+  *pipe = nullptr;
+  const size_t esz = esize(dtype);
+  if (!esz) return fail(hipErrorInvalidValue, "host_pipe_create: unknown dtype");
+  if (depth < 0 || depth > 8) return fail(hipErrorInvalidValue, "host_pipe_create: depth must be 0..8");
+  if (!chunk_bytes) chunk_bytes = kPipeChunkBytes;
+  if (chunk_bytes < esz) return fail(hipErrorInvalidValue, "host_pipe_create: chunk_bytes below one element");
+  int ndev = 0;
+  if (int e = check_hip(hipGetDeviceCount(&ndev), "host_pipe_create: hipGetDeviceCount")) return e;
+  if (device < 0 || device >= ndev) return fail(hipErrorInvalidDevice, "host_pipe_create: bad device");
+  if (int e = check_hip(hipSetDevice(device), "host_pipe_create: hipSetDevice")) return e;
+  auto *p = new hiccl_host_pipe;
+  p->dtype = dtype;
+  p->device = device;
+  p->esz = esz;
+  p->chunk = chunk_bytes / esz;
+  p->depth = depth ? depth : kPipeDepth;
+  p->stage.assign(p->depth, nullptr);
+  for (int i = 0; i < p->depth; i++) {
+    hipStream_t s = nullptr;
+    if (int e = check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "host_pipe_create: stream")) {
+      hiccl_host_pipe_destroy(p);
+      return e;
+    }
+    p->streams.push_back(s);
+  }
+  *pipe = p;
+  return 0;
+}
+
+int hiccl_host_pipe_reduce(hiccl_host_pipe_t *p, void *out, const void *const *in, int n, size_t count) {
+  if (!p) return fail(hipErrorInvalidValue, "host_pipe_reduce: pipe is NULL");
+  if (p->dtype == HICCL_BYTES && n != 1) return fail(hipErrorInvalidValue, "host_pipe_reduce: HICCL_BYTES copies need n == 1");
+  if (int e = check_buffers(out, in, n, count, p->esz)) return e;
+  if (count == 0) return 0;
+  if (int e = check_hip(hipSetDevice(p->device), "host_pipe_reduce: hipSetDevice")) return e;
+  if (int e = pipe_stage_for(p, n)) return e;
+  const size_t slot_in = p->chunk * p->esz;  // bytes between staged inputs
+  std::vector<const void *> dev_in((size_t)(n > 0 ? n : 1));
+  int err = 0;
+  size_t c = 0;
+  for (size_t lo = 0; lo < count && !err; lo += p->chunk, c++) {
+    const size_t len = count - lo < p->chunk ? count - lo : p->chunk;
+    const int slot = (int)(c % (size_t)p->depth);
+    hipStream_t s = p->streams[slot];
+    char *stage = p->stage[slot];
+    for (int k = 0; k < n && !err; k++) {
+      dev_in[k] = stage + (size_t)k * slot_in;
+      err = check_hip(hipMemcpyAsync(stage + (size_t)k * slot_in, (const char *)in[k] + lo * p->esz,
+                                     len * p->esz, hipMemcpyHostToDevice, s),
+                      "host_pipe_reduce: H2D");
+    }
+    // in place into staged input 0 (exact aliasing is element-wise safe)
+    if (!err) err = hiccl_reduce_ex(p->dtype, stage, dev_in.data(), n, len, s, nullptr);
+    if (!err)
+      err = check_hip(hipMemcpyAsync((char *)out + lo * p->esz, stage, len * p->esz, hipMemcpyDeviceToHost, s),
+                      "host_pipe_reduce: D2H");
+  }
+  for (hipStream_t s : p->streams) {  // drain every slot, even after an error
+    int e = check_hip(hipStreamSynchronize(s), "host_pipe_reduce: sync");
+    if (!err) err = e;
+  }
+  return err;
+}
+
+void hiccl_host_pipe_destroy(hiccl_host_pipe_t *p) {
+  if (!p) return;
+  (void)hipSetDevice(p->device);
+  for (hipStream_t s : p->streams) (void)hipStreamSynchronize(s);
+  for (char *b : p->stage)
+    if (b) (void)hipFree(b);
+  for (hipStream_t s : p->streams) (void)hipStreamDestroy(s);
   delete p;
 }
 

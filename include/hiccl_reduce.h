@@ -184,6 +184,34 @@ size_t hiccl_reduce_plan_bytes(const hiccl_reduce_plan_t *plan);
 void hiccl_reduce_plan_destroy(hiccl_reduce_plan_t *plan);
 
 /* ----------------------------------------------------------------------
+ * Host-resident buckets.
+ *
+ * The reference reduces host arrays with its host port (reduce_kernel,
+ * compute.h:14-23) and stages host<->device copies around the device path
+ * in its benchmarks (bench.h:80-108).  A host pipe reduces n host-resident
+ * inputs into a host-resident output on the GPU: the bucket is cut into
+ * chunks of chunk_bytes per input; chunk c's n H2D copies, its reduction
+ * (hiccl_reduce, in place into the staged input 0) and its D2H copy run on
+ * stream c % depth, so the two PCIe directions and the kernel overlap.
+ * Same bits as hiccl_reduce on the same inputs.  Pinned memory
+ * (hipHostMalloc / hipHostRegister) is needed for the overlap; pageable
+ * memory gives the same result with serialised copies.
+ *   create   chunk_bytes 0 = 64 MiB per input; depth 0 = 3 (1..8 allowed);
+ *            device staging (depth x n x chunk_bytes) is allocated on the
+ *            first reduce and grows with n.
+ *   reduce   blocking: returns when out holds the sum.  Pointers must be
+ *            element-aligned; partial overlaps are refused.
+ *   destroy  frees staging and streams.
+ */
+typedef struct hiccl_host_pipe hiccl_host_pipe_t;
+
+int hiccl_host_pipe_create(hiccl_host_pipe_t **pipe, int dtype, int device, size_t chunk_bytes,
+                           int depth);
+int hiccl_host_pipe_reduce(hiccl_host_pipe_t *pipe, void *out, const void *const *in, int n,
+                           size_t count);
+void hiccl_host_pipe_destroy(hiccl_host_pipe_t *pipe);
+
+/* ----------------------------------------------------------------------
  * Stream-ordered signalling for the transport (include/hiccl/transport.h).
  *
  * Enqueues on `stream` (after all earlier work on it): a system-scope

@@ -80,6 +80,16 @@ def test_invalid_arguments_rejected_on_host():
     assert lib.hiccl_reduce_plan_engine(None) == -1
     assert lib.hiccl_reduce_plan_numcomp(None) == 0
     lib.hiccl_reduce_plan_destroy(None)
+    # host pipe: argument checks come before any HIP call
+    h = ctypes.c_void_p()
+    assert lib.hiccl_host_pipe_create(None, 0, 0, 0, 0) == 1
+    assert lib.hiccl_host_pipe_create(ctypes.byref(h), 42, 0, 0, 0) == 1 and not h.value
+    assert "dtype" in L.last_error()
+    assert lib.hiccl_host_pipe_create(ctypes.byref(h), 0, 0, 0, 9) == 1
+    assert "depth" in L.last_error()
+    assert lib.hiccl_host_pipe_create(ctypes.byref(h), 1, 0, 4, 0) == 1  # f64 chunk < 1 element
+    assert lib.hiccl_host_pipe_reduce(None, ctypes.c_void_p(0x1000), _tab([0x2000]), 1, 4) == 1
+    lib.hiccl_host_pipe_destroy(None)
 
 
 def test_python_layer_refuses_cpu_tensors():

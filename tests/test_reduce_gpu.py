@@ -405,6 +405,41 @@ def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
         comp.close()
 
 
+def test_plan_auto_engine_bf16():
+    """bf16 with >= 5 inputs: AUTO takes TILE only from 64 tickets per
+    workgroup (n = 8: 2^27 elements per input on 256 CUs), PHASE below;
+    either engine gives the other's bits, and the TILE result matches an
+    in-order bf16 sum on the host (sampled)."""
+    P, T = hiccl_amd.HICCL_ENGINE_PHASE, hiccl_amd.HICCL_ENGINE_TILE
+    big = 1 << 27
+    base = torch.empty(big + 64, dtype=torch.bfloat16, device=DEV)
+    hiccl_amd.fill_uniform(base, 91, 0)
+    offs = (0, 0, 1, 3, 0, 2, 7, 5)
+    full = 256 == torch.cuda.get_device_properties(0).multi_processor_count
+    for cnt, expect, other in ((big, T, P), (big // 2, P, T)):
+        ins = [(base, o) for o in offs]
+        outs = []
+        for eng in (hiccl_amd.HICCL_ENGINE_AUTO, other):
+            out = torch.empty(cnt, dtype=torch.bfloat16, device=DEV)
+            comp = hiccl_amd.Compute(torch.bfloat16, device=0, engine=eng)
+            comp.add(ins, out, cnt, compid=0)
+            comp.start()
+            comp.wait()
+            if eng == hiccl_amd.HICCL_ENGINE_AUTO and full:
+                assert comp.engine() == expect
+            comp.close()
+            outs.append(out)
+        assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+        idx = torch.randint(0, cnt, (4096,), generator=torch.Generator().manual_seed(cnt % 97))
+        host = base.cpu()
+        acc = torch.zeros(idx.numel(), dtype=torch.bfloat16)
+        for o in offs:  # reduce_kernel<T>: T acc = 0; acc += in[k][i] (compute.h:2-12)
+            acc = (acc.float() + host[idx + o].float()).to(torch.bfloat16)
+        got = outs[0][idx.to(DEV)].cpu()
+        assert torch.equal(got.view(torch.int16), acc.view(torch.int16))
+        del outs
+
+
 def test_plan_launch_from_other_thread(oracle):
     """Comm::start runs compute->start() on a pthread (comm.h:214-224)."""
     import threading
