@@ -319,6 +319,7 @@ def main():
     ap.add_argument("--crossover", action="store_true")
     ap.add_argument("--planvs", action="store_true")
     ap.add_argument("--schedsweep", action="store_true")
+    ap.add_argument("--sweepset", default="", help="schedsweep: '' (schedule/grab) | occupancy")
     ap.add_argument("--xdtype", default="both", help="crossover: f32 | bf16 | both")
     ap.add_argument("--xmib", default="", help="crossover: comma list of MiB per input")
     ap.add_argument("--xn", default="", help="crossover: comma list of input counts")
@@ -503,11 +504,39 @@ def schedsweep(args):
     cases = ((2, 256), (2, 1024), (4, 256), (4, 1024), (8, 256), (8, 1024), (16, 256))
     if args.buckets:
         cases = ((args.n, (1 << args.log2count) * 4 >> 20),) * args.buckets
+    elif args.xmib:
+        ns = [int(v) for v in args.xn.split(",")] if args.xn else [args.n]
+        cases = tuple((n, int(m)) for n in ns for m in args.xmib.split(","))
     variants = [("tile_static", dict(engine=1, schedule=1)), ("tile_dyn_g1", dict(engine=1, schedule=2, grab=1)),
                 ("tile512_dyn_g1", dict(engine=1, schedule=2, grab=1, block=512, unroll=4)),
                 ("tile_dyn_g2", dict(engine=1, schedule=2, grab=2)),
                 ("phase_static", dict(engine=2, schedule=1)), ("phase_dyn_g1", dict(engine=2, schedule=2, grab=1)),
                 ("auto", None)]
+    if args.sweepset == "occupancy":  # C2-shaped: workgroups per CU / tile shape on the dynamic schedule
+        variants = [("auto", None),
+                    ("t256x4_bpc2_g1", dict(engine=1, schedule=2, grab=1, blocks_per_cu=2)),
+                    ("t256x4_bpc2_g2", dict(engine=1, schedule=2, grab=2, blocks_per_cu=2)),
+                    ("t512x2_g1", dict(engine=1, schedule=2, grab=1, block=512, unroll=2)),
+                    ("t512x2_bpc2_g1", dict(engine=1, schedule=2, grab=1, block=512, unroll=2, blocks_per_cu=2)),
+                    ("t256x2_bpc2_g2", dict(engine=1, schedule=2, grab=2, unroll=2, blocks_per_cu=2)),
+                    ("t256x2_g2", dict(engine=1, schedule=2, grab=2, unroll=2)),
+                    ("t256x4_g1_drain", dict(engine=1, schedule=2, grab=1, drain=1))]
+    if args.sweepset == "small":  # few tiles per workgroup: more workgroups / smaller tiles
+        variants = [("auto", None),
+                    ("t256x4_bpc2", dict(engine=1, blocks_per_cu=2)),
+                    ("t256x4_bpc4", dict(engine=1, blocks_per_cu=4)),
+                    ("t256x2", dict(engine=1, unroll=2)),
+                    ("t256x2_bpc2", dict(engine=1, unroll=2, blocks_per_cu=2)),
+                    ("t256x1_bpc4", dict(engine=1, unroll=1, blocks_per_cu=4)),
+                    ("t256x4_dyn", dict(engine=1, schedule=2, grab=1)),
+                    ("phase", dict(engine=2))]
+    if args.sweepset == "xover":  # engine x schedule crossover (sets AUTO)
+        variants = [("auto", None),
+                    ("tile_dyn", dict(engine=1, schedule=2)),
+                    ("tile_static", dict(engine=1, schedule=1)),
+                    ("tile_bpc4_static", dict(engine=1, schedule=1, blocks_per_cu=4)),
+                    ("phase_static", dict(engine=2, schedule=1)),
+                    ("phase_dyn", dict(engine=2, schedule=2))]
     for n, mib in cases:
         count = (mib << 20) // 4
         ins, out = make_bucket(n, count)

@@ -722,8 +722,9 @@ constexpr double kDynMinInputs = 5;
 // ((n + 1) per tile): one tile at n >= 8, two at n = 4..7, ... -- a ticket
 // costs an atomic and a workgroup barrier (profiles/r01_schedsweep*.jsonl).
 constexpr double kTicketTiles = 9;
-// bf16 takes the tile engine (AUTO) only from this many tickets per workgroup.
-constexpr uint64_t kBf16TileMinTicketsPerWG = 64;
+// AUTO takes the tile engine (n >= kDynMinInputs) from this many tickets per
+// workgroup on: below it the phased engine is ahead.
+constexpr uint64_t kTileMinTicketsPerWG = 64;
 
 // Units per ticket of the dynamic schedule: one 128 KiB phased chunk; for
 // tiles enough to cover kTicketTiles tile-loads.
@@ -831,6 +832,7 @@ constexpr int kDefBlock = 256;
 constexpr int kDefUnroll = 4;
 constexpr int kDefPol = 11;  // nt loads, nt stores
 constexpr int kDefBpc = 1;
+constexpr int kSmallBpc = 4;
 constexpr int kPhBlock = 512;
 // auto engine: with >= 5 inputs the TILE engine on the dynamic schedule;
 // with fewer, PHASE (static) when every CU gets a chunk, else TILE
@@ -857,7 +859,7 @@ struct Cfg {
 
 // Raw config: zero block/unroll stay zero until the engine is known.
 Cfg resolve(const hiccl_reduce_config_t *c) {
-  Cfg r{0, 0, kDefBpc, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO, HICCL_SCHED_AUTO, 0, 0};
+  Cfg r{0, 0, 0, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO, HICCL_SCHED_AUTO, 0, 0};
   if (c) {
     r.block = c->block;
     r.unroll = c->unroll;
@@ -876,20 +878,32 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
 
 // Auto engine from the packets per input of a launch (summed over its
 // computes) and the number of inputs (packet-weighted mean for a plan).
+// Interleaved engine x schedule sweeps, n = 5 / 8 / 16 x 32 MiB-1 GiB per
+// input (profiles/r01g_xover.jsonl; bf16: r01g_bf16_crossover.jsonl): the
+// tile engine on the dynamic schedule leads from 64 tickets per workgroup
+// (n = 8, 1 GiB: 6.71 vs 6.32 TB/s phased), the phased engine below it
+// (n = 8, 128 MiB = 32 tickets: 6.41 vs 5.94); with <= 4 inputs the phased
+// engine leads at every size with a chunk per CU (r01_schedsweep.jsonl).
 int auto_engine(uint64_t npkt, double n, int dtype, int acc, int dev) {
-  if (n >= kDynMinInputs) {
-    if (dtype != HICCL_BFLOAT16) return HICCL_ENGINE_TILE;
-    // bf16 (packed accumulator) adds 3x the VALU work per tile: the tile
-    // engine needs more tickets per workgroup before it passes the phased
-    // one (n = 8: 128 MiB per input 6.00 vs 6.28, 256 MiB 6.38 vs 6.23,
-    // 1 GiB 6.50 vs 6.09 TB/s; profiles/r01g_bf16_crossover.jsonl)
+  const bool packed_ok = !(dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_WIDE);
+  if (n >= kDynMinInputs && packed_ok) {
     const uint64_t tickets = npkt / ((uint64_t)kDefBlock * kDefUnroll) / default_grab(HICCL_ENGINE_TILE, n);
-    if (acc == HICCL_ACC_NATIVE && tickets >= kBf16TileMinTicketsPerWG * (uint64_t)device_cus(dev))
-      return HICCL_ENGINE_TILE;
+    if (tickets >= kTileMinTicketsPerWG * (uint64_t)device_cus(dev)) return HICCL_ENGINE_TILE;
   }
   const uint64_t chunk = (uint64_t)kPhBlock * phase_p_dtype(dtype, acc);
   return npkt >= kPhaseMinChunksPerCU * (uint64_t)device_cus(dev) * chunk ? HICCL_ENGINE_PHASE
                                                                           : HICCL_ENGINE_TILE;
+}
+
+// Workgroups per CU: a tile launch too small for a phased chunk per CU has
+// few tiles per workgroup and is latency-bound -- four workgroups per CU
+// keep more of it in flight (n = 8, 16 MiB per input: 6.31 vs 6.01 TB/s,
+// 32 MiB: 6.27-6.40 vs 5.97-6.13; profiles/r01g_small_sweep.jsonl).
+int auto_bpc(int engine, uint64_t npkt, int dtype, int acc, int dev) {
+  const uint64_t chunk = (uint64_t)kPhBlock * phase_p_dtype(dtype, acc);
+  return engine == HICCL_ENGINE_TILE && npkt < kPhaseMinChunksPerCU * (uint64_t)device_cus(dev) * chunk
+             ? kSmallBpc
+             : kDefBpc;
 }
 
 // Fill in the engine and its default shape.
@@ -903,6 +917,7 @@ void finish_cfg(Cfg &c, uint64_t npkt, int n, int dtype, int dev) {
     if (!c.block) c.block = kDefBlock;
     if (!c.unroll) c.unroll = kDefUnroll;
   }
+  if (!c.bpc) c.bpc = auto_bpc(c.engine, npkt, dtype, c.acc, dev);
 }
 
 // ---- single-compute dispatch (template instantiation table)
@@ -1139,6 +1154,7 @@ struct hiccl_reduce_plan {
   int engine_req = HICCL_ENGINE_AUTO;  // hiccl_reduce_plan_set_engine
   int engine = HICCL_ENGINE_TILE;      // resolved at upload
   double mean_n = 0;                   // packet-weighted inputs per compute
+  int bpc = 1;                         // workgroups per CU, resolved at upload
   size_t esz = 0;
   struct Comp {
     void *out;
@@ -1188,6 +1204,7 @@ int plan_upload(hiccl_reduce_plan *p) {
   p->engine = p->engine_req != HICCL_ENGINE_AUTO
                   ? p->engine_req
                   : auto_engine(total_pkt, mean_n, p->dtype, p->acc, p->device);
+  p->bpc = auto_bpc(p->engine, total_pkt, p->dtype, p->acc, p->device);
   const uint64_t unit = unit_pkts(p->engine, p->dtype, p->acc);
   uint64_t tile = 0;
   size_t off = 0;
@@ -1222,7 +1239,7 @@ int plan_kernel(hiccl_reduce_plan *p, uint32_t c0, uint64_t t0, uint64_t t1, int
                 hipStream_t s) {
   plan_fn fn = pick_plan(p->dtype, p->acc, p->engine);
   if (!fn) return fail(hipErrorInvalidValue, "plan: unsupported dtype");
-  uint64_t grid = (uint64_t)device_cus(p->device) * kPlanBpc;
+  uint64_t grid = (uint64_t)device_cus(p->device) * p->bpc;
   if (grid > t1 - t0) grid = t1 - t0;
   fn(p->d_desc, c0, (uint32_t)p->comps.size(), t0, t1,
      unit_sched_for(p->engine, p->mean_n, t1 - t0, grid, p->device, s), default_grab(p->engine, p->mean_n),

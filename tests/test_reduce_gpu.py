@@ -380,15 +380,17 @@ def test_plan_phase_engine(oracle, each):
 
 
 def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
-    """AUTO resolves to TILE with >= 5 inputs; with fewer, to PHASE once
-    every CU gets a chunk of 128 KiB (f32: 2^23 elements per input on 256
-    CUs), to TILE below."""
+    """AUTO resolves to TILE with >= 5 inputs from 64 tickets per workgroup
+    (n = 6: two tiles per ticket, 2^27 f32 per input on 256 CUs); otherwise
+    to PHASE once every CU gets a chunk of 128 KiB (f32: 2^23 elements per
+    input), to TILE below."""
     count = 1 << 23
-    a = torch.empty(count, device=DEV)
+    a = torch.empty(1 << 27, device=DEV)
     hiccl_amd.fill_uniform(a, 77, 0)
-    out = torch.empty(count, device=DEV)
+    out = torch.empty(1 << 27, device=DEV)
     P, T = hiccl_amd.HICCL_ENGINE_PHASE, hiccl_amd.HICCL_ENGINE_TILE
-    for cnt, n, expect in ((count, 6, T), (count, 2, P), (count // 4, 6, T), (count // 4, 2, T)):
+    for cnt, n, expect in ((1 << 27, 6, T), (1 << 26, 6, P), (count, 6, P), (count, 2, P), (count // 4, 6, T),
+                           (count // 4, 2, T)):
         comp = hiccl_amd.Compute(torch.float32, device=0)
         comp.add([a] * n, out, cnt, compid=0)
         comp.start()
