@@ -95,6 +95,9 @@ _SIGS = {
     "hiccl_stream_copy": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
     "hiccl_signal_wait": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_uint32, _vp,
                                          ctypes.c_double, _vp]),
+    "hiccl_signal_wait_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_uint32, _vp, _vp,
+                                             ctypes.c_double, _vp]),
+    "hiccl_counter_add": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp]),
 }
 
 

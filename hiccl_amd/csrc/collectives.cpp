@@ -126,9 +126,15 @@ int main(int argc, char *argv[]) {
       for (size_t i = 0; i < in.size(); i++) in[i] = (Type)uniform_f32(1234, (uint32_t)myid, i);
       CommBench::memcpyH2D(sendbuf_d, in.data(), in.size());
       std::vector<Type> nanfill(count * numproc, (Type)-1);
-      CommBench::memcpyH2D(recvbuf_d, nanfill.data(), nanfill.size());
-      MPI_Barrier(CommBench::comm_mpi);
-      coll.run();
+      // HICCL_DRIVER_REPEAT=k: k runs, the receive buffer refilled before
+      // each (graph mode: eager, capture + replay, replays), last one dumped
+      const char *rep = std::getenv("HICCL_DRIVER_REPEAT");
+      const int repeat = rep && std::atoi(rep) > 1 ? std::atoi(rep) : 1;
+      for (int r = 0; r < repeat; r++) {
+        CommBench::memcpyH2D(recvbuf_d, nanfill.data(), nanfill.size());
+        MPI_Barrier(CommBench::comm_mpi);
+        coll.run();
+      }
       std::vector<Type> out(count * numproc);
       CommBench::memcpyD2H(out.data(), recvbuf_d, out.size());
       std::string path = std::string(dump) + ".rank" + std::to_string(myid) + ".bin";

@@ -659,16 +659,19 @@ struct SigWaitArgs {
   uint32_t *sig[kMaxFlags];
   const uint32_t *wait[kMaxFlags];
   uint32_t *err;
+  const uint32_t *epoch_dev;  // NULL, or a device word added to epoch at run time (graph replays)
   uint64_t timeout_ticks;
   uint32_t nsig, nwait, epoch, pad;
 };
 
 __global__ __launch_bounds__(64) void k_sigwait(SigWaitArgs a) {
   const uint32_t lane = threadIdx.x;
-  if (lane < a.nsig) __hip_atomic_store(a.sig[lane], a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint32_t epoch = a.epoch;
+  if (a.epoch_dev) epoch += __hip_atomic_load(a.epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane < a.nsig) __hip_atomic_store(a.sig[lane], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (lane < a.nwait) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int32_t)(__hip_atomic_load(a.wait[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - a.epoch) < 0) {
+    while ((int32_t)(__hip_atomic_load(a.wait[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       __builtin_amdgcn_s_sleep(2);
       // an earlier timeout (any wait of this rank) ends every later spin at once
       if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
@@ -678,6 +681,11 @@ __global__ __launch_bounds__(64) void k_sigwait(SigWaitArgs a) {
       }
     }
   }
+}
+
+// One lane adds v to a device counter (stream-ordered; graph replay number).
+__global__ __launch_bounds__(64) void k_counter_add(uint32_t *ctr, uint32_t v) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------ host side ----
@@ -1348,6 +1356,10 @@ int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *p, void *stream) {
   if (int e = plan_upload(p)) return e;
   hipStream_t s = (hipStream_t)stream;
   if (int e = plan_kernel(p, 0, 0, p->total_tiles, p->maxn, s)) return e;
+  // a capturing stream gets no completion event (plan_sync does not apply
+  // to graph replays: synchronise the stream the graph runs on)
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) return 0;
   p->launched = true;
   return check_hip(hipEventRecord(p->done, s), "plan_launch: event");
 }
@@ -1523,6 +1535,18 @@ void hiccl_host_pipe_destroy(hiccl_host_pipe_t *p) {
 
 int hiccl_signal_wait(uint32_t *const *sig, int nsig, const uint32_t *const *wait, int nwait,
                       uint32_t epoch, uint32_t *err, double timeout_s, void *stream) {
+  return hiccl_signal_wait_dev(sig, nsig, wait, nwait, epoch, nullptr, err, timeout_s, stream);
+}
+
+int hiccl_counter_add(uint32_t *ctr, uint32_t v, void *stream) {
+  if (!ctr) return fail(hipErrorInvalidValue, "counter_add: ctr is NULL");
+  hipLaunchKernelGGL(k_counter_add, dim3(1), dim3(64), 0, (hipStream_t)stream, ctr, v);
+  return check_hip(hipGetLastError(), "counter_add: launch");
+}
+
+int hiccl_signal_wait_dev(uint32_t *const *sig, int nsig, const uint32_t *const *wait, int nwait,
+                          uint32_t epoch, const uint32_t *epoch_dev, uint32_t *err, double timeout_s,
+                          void *stream) {
   if (nsig < 0 || nwait < 0 || (nsig && !sig) || (nwait && !wait))
     return fail(hipErrorInvalidValue, "signal_wait: bad flag lists");
   const uint64_t ticks = (uint64_t)((timeout_s > 0 ? timeout_s : 30.0) * 1e8);  // s_memrealtime: 100 MHz
@@ -1532,6 +1556,7 @@ int hiccl_signal_wait(uint32_t *const *sig, int nsig, const uint32_t *const *wai
     SigWaitArgs a;
     memset(&a, 0, sizeof(a));
     a.err = err;
+    a.epoch_dev = epoch_dev;
     a.timeout_ticks = ticks;
     a.epoch = epoch;
     for (; i < nsig && a.nsig < (uint32_t)kMaxFlags; i++) {

@@ -132,6 +132,15 @@ class Comm {
   // the reduction kernel reads the sender's buffer over xGMI in place.
   // Opt-in (HICCL_FUSED_GATHER=1 or this setter); results are identical.
   void set_fused_gather(bool on) { fuse_req = on ? 1 : 0; }
+  // hipGraph replay of stream-ordered runs (HIP port; needs stream-ordered
+  // mode): the first run() executes eagerly (uploads every plan), the second
+  // captures the whole enqueued pipeline into a graph, and every run()
+  // replays it -- one hipGraphLaunch instead of a few launches per step.
+  // The signal epochs come from a device counter the graph bumps first
+  // (hiccl_signal_wait_dev).  Opt-in (HICCL_GRAPH=1 or this setter); every
+  // rank must agree (init reduces the choice).
+  void set_graph(bool on) { graph_req = on ? 1 : 0; }
+  bool graph_mode() const { return graphed; }
   void set_endpoints(T *sb, size_t sc, T *rb, size_t rc) {
     sendbuf = sb;
     sendcount = sc;
@@ -214,6 +223,7 @@ class Comm {
     steps = merge_steps(coll_batch, libs, 1);
     streamed = want_stream_mode();
     fused = want_fused();
+    graphed = streamed && want_graph();
     CommBench::stream_ordered = streamed;
     command_batch = instantiate(steps, libs, fused);
     CommBench::stream_ordered = false;
@@ -237,8 +247,9 @@ class Comm {
     MPI_Barrier(CommBench::comm_mpi);  // nobody runs before every rank's handles are exchanged
     report_memory();
     if (CommBench::myid == CommBench::printid)
-      std::printf("initialization time: %e seconds (%zu steps, %zu libraries, %s%s)\n", MPI_Wtime() - t0, steps.size(),
-                  libs.size(), streamed ? "stream-ordered" : "host-driven", fused ? ", fused gather" : "");
+      std::printf("initialization time: %e seconds (%zu steps, %zu libraries, %s%s%s)\n", MPI_Wtime() - t0,
+                  steps.size(), libs.size(), streamed ? "stream-ordered" : "host-driven", graphed ? ", graph replay" : "",
+                  fused ? ", fused gather" : "");
   }
 
   bool stream_ordered() const { return streamed; }
@@ -338,6 +349,8 @@ class Comm {
   bool streamed = false;
   int fuse_req = -1;  // -1: HICCL_FUSED_GATHER
   bool fused = false;
+  int graph_req = -1;  // -1: HICCL_GRAPH
+  bool graphed = false;
 #ifndef HICCL_PORT_HOST
   CommBench::FlagSpace flags;
 
@@ -347,10 +360,25 @@ class Comm {
   void run_streamed() {
     CommBench::setup_gpu();
     hipStream_t s = CommBench::transport_stream();
+    if (command_batch.empty()) return;
+    if (graphed && ran_eager) {
+      if (gexec && !epochs_match()) drop_graph();  // eager executions since (measure): re-record
+      if (!gexec) capture(s);
+      CommBench::hip_check(hipGraphLaunch(gexec, s), "run: hipGraphLaunch");
+      for_each_comm([](CommBench::Comm<T> &c) { c.replayed(); });
+      replays++;
+    } else {
+      enqueue_pipeline(s);
+      ran_eager = true;
+    }
+    CommBench::hip_check(hipStreamSynchronize(s), "run: stream sync");
+    if (*flags.err) CommBench::die("run", "stream-ordered signal timed out (a peer never signalled)");
+  }
+
+  void enqueue_pipeline(hipStream_t s) {
     const size_t nl = command_batch.size();
     std::vector<typename std::list<Command<T>>::iterator> it(nl);
     for (size_t i = 0; i < nl; i++) it[i] = command_batch[i].begin();
-    if (nl == 0) return;
     while (it[0] != command_batch[0].end()) {
       for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
       for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
@@ -359,10 +387,80 @@ class Comm {
         ++it[i];
       }
     }
-    CommBench::hip_check(hipStreamSynchronize(s), "run: stream sync");
-    if (*flags.err) CommBench::die("run", "stream-ordered signal timed out (a peer never signalled)");
   }
+
+  template <class F>
+  void for_each_comm(F f) {
+    for (auto &lst : command_batch)
+      for (auto &c : lst) f(*c.comm);
+  }
+
+  // Record the pipeline once: replay counter bump, then the same enqueue
+  // sequence with every wait reading its epoch through the counter.  The
+  // plans were uploaded by the eager run; their launches take the static
+  // unit schedule while the stream captures (no shared ticket counter in a
+  // replayable graph).
+  void capture(hipStream_t s) {
+    CommBench::hip_check(hipMalloc((void **)&graph_ctr, sizeof(uint32_t)), "graph: hipMalloc counter");
+    CommBench::hip_check(hipMemset(graph_ctr, 0, sizeof(uint32_t)), "graph: hipMemset counter");
+    CommBench::hip_check(hipDeviceSynchronize(), "graph: sync");
+    CommBench::hip_check(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "graph: begin capture");
+    if (hiccl_counter_add(graph_ctr, 1, s)) CommBench::die("graph: counter", hiccl_last_error());
+    for_each_comm([this](CommBench::Comm<T> &c) { c.begin_capture(graph_ctr); });
+    enqueue_pipeline(s);
+    for_each_comm([](CommBench::Comm<T> &c) { c.end_capture(); });
+    graph_base.clear();
+    for_each_comm([this](CommBench::Comm<T> &c) { graph_base.push_back(c.epoch_now()); });
+    replays = 0;
+    hipGraph_t g = nullptr;
+    CommBench::hip_check(hipStreamEndCapture(s, &g), "graph: end capture");
+    CommBench::hip_check(hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0), "graph: instantiate");
+    CommBench::hip_check(hipGraphDestroy(g), "graph: destroy");
+  }
+
+  // The graph's waits use (epoch at capture) + replay number: valid while no
+  // eager execution (Comm::measure) advanced a transport's epoch since.
+  bool epochs_match() {
+    size_t i = 0;
+    bool ok = true;
+    for_each_comm([&](CommBench::Comm<T> &c) { ok = ok && c.epoch_now() == graph_base[i++] + replays; });
+    return ok;
+  }
+  void drop_graph() {
+    CommBench::hip_check(hipGraphExecDestroy(gexec), "graph: destroy exec");
+    CommBench::hip_check(hipFree(graph_ctr), "graph: free counter");
+    gexec = nullptr;
+    graph_ctr = nullptr;
+  }
+
+  bool ran_eager = false;
+  uint32_t *graph_ctr = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  std::vector<uint32_t> graph_base;
+  uint32_t replays = 0;
+
+ public:
+  ~Comm() {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (graph_ctr) (void)hipFree(graph_ctr);
+  }
+
+ private:
 #endif
+
+  bool want_graph() {
+#ifdef HICCL_PORT_HOST
+    return false;
+#else
+    int on = graph_req;
+    if (on < 0) {
+      const char *env = std::getenv("HICCL_GRAPH");
+      on = (env && std::string(env) == "1") ? 1 : 0;
+    }
+    MPI_Allreduce(MPI_IN_PLACE, &on, 1, MPI_INT, MPI_LAND, CommBench::comm_mpi);
+    return on != 0;
+#endif
+  }
 
   bool want_stream_mode() {
 #ifdef HICCL_PORT_HOST

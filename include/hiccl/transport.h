@@ -299,11 +299,12 @@ inline double signal_timeout() {
   return t;
 }
 
+// epoch_dev != NULL (graph capture): the epoch used is epoch + *epoch_dev at run time.
 inline void signal_wait(const std::vector<uint32_t *> &sig, const std::vector<uint32_t *> &wait, uint32_t epoch,
-                        uint32_t *err, hipStream_t stream) {
+                        const uint32_t *epoch_dev, uint32_t *err, hipStream_t stream) {
   if (sig.empty() && wait.empty()) return;
-  int e = hiccl_signal_wait(sig.data(), (int)sig.size(), (const uint32_t *const *)wait.data(), (int)wait.size(), epoch,
-                            err, signal_timeout(), stream);
+  int e = hiccl_signal_wait_dev(sig.data(), (int)sig.size(), (const uint32_t *const *)wait.data(), (int)wait.size(),
+                                epoch, epoch_dev, err, signal_timeout(), stream);
   if (e) die("hiccl_signal_wait", hiccl_last_error());
 }
 #endif
@@ -439,11 +440,24 @@ class Comm {
   // done tokens of fused transfers follow the step's compute: enqueue_tail.
   void enqueue(hipStream_t s) {
     ++epoch;
-    signal_wait(pre_sig, pre_wait, epoch, flags->err, s);
+    signal_wait(pre_sig, pre_wait, sig_epoch(), graph_epoch, flags->err, s);
     launch_copies(s);
-    signal_wait(post_sig, post_wait, epoch, flags->err, s);
+    signal_wait(post_sig, post_wait, sig_epoch(), graph_epoch, flags->err, s);
   }
-  void enqueue_tail(hipStream_t s) { signal_wait(tail_sig, tail_wait, epoch, flags->err, s); }
+  void enqueue_tail(hipStream_t s) { signal_wait(tail_sig, tail_wait, sig_epoch(), graph_epoch, flags->err, s); }
+
+  // hipGraph capture of stream-ordered executions (HiCCL::Comm::run with
+  // HICCL_GRAPH=1): while `ctr` is set, every wait is enqueued as
+  // (epoch before this execution) + *ctr, where *ctr is the replay number
+  // (1, 2, ...) bumped by the graph's first node; the host epoch then
+  // advances by one per replay (end_capture undoes the capture's own ++).
+  void begin_capture(const uint32_t *ctr) { graph_epoch = ctr; }
+  void end_capture() {
+    graph_epoch = nullptr;
+    --epoch;
+  }
+  void replayed() { ++epoch; }
+  uint32_t epoch_now() const { return epoch; }
 
   bool stream_mode() const { return streamed; }
 #endif
@@ -613,6 +627,8 @@ class Comm {
   bool streamed = false;
   FlagSpace *flags = nullptr;
   uint32_t epoch = 0;
+  const uint32_t *graph_epoch = nullptr;  // set while a graph is being captured
+  uint32_t sig_epoch() const { return graph_epoch ? epoch - 1 : epoch; }
   std::vector<uint32_t *> pre_sig, pre_wait, post_sig, post_wait, tail_sig, tail_wait;
   // batched exact copies (HICCL_BYTES plans): the bytes this rank moves to or
   // from peers, and its self transfers -- one kernel each per execution

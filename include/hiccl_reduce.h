@@ -54,10 +54,11 @@ typedef enum {
  *   PHASE  a workgroup sweeps a 128 KiB chunk of input 0, then of input 1,
  *          ... (next input's loads in flight while the current one is
  *          added), then writes the chunk.
- *   AUTO   TILE (on the dynamic schedule, below) with >= 5 inputs, except
- *          bf16; otherwise PHASE when every CU gets >= 1 chunk, else TILE
- *          (one-shot: that call; plan: all computes, packet-weighted mean
- *          n). */
+ *   AUTO   TILE (on the dynamic schedule, below) with >= 5 inputs once
+ *          every workgroup gets >= 64 tickets (bf16: packed accumulator
+ *          only); otherwise PHASE when every CU gets >= 1 chunk, else TILE
+ *          with 4 workgroups per CU (one-shot: that call; plan: all
+ *          computes, packet-weighted mean n). */
 typedef enum {
   HICCL_ENGINE_AUTO = 0,
   HICCL_ENGINE_TILE = 1,
@@ -72,7 +73,7 @@ typedef enum {
  *   AUTO     DYNAMIC for the TILE engine with >= 5 inputs and >= 32 tickets
  *            per workgroup, STATIC otherwise and always during stream
  *            capture.  A forced DYNAMIC still needs >= 32 tickets per
- *            workgroup. 
+ *            workgroup.
  * Plans use AUTO. */
 typedef enum {
   HICCL_SCHED_AUTO = 0,
@@ -225,6 +226,14 @@ void hiccl_host_pipe_destroy(hiccl_host_pipe_t *pipe);
  */
 int hiccl_signal_wait(uint32_t *const *sig, int nsig, const uint32_t *const *wait, int nwait,
                       uint32_t epoch, uint32_t *err, double timeout_s, void *stream);
+/* Graph-replayable form: the epoch used is epoch + *epoch_dev, read when the
+ * wait runs (epoch_dev NULL: epoch alone), so a captured hipGraph advances
+ * its epochs through a device counter bumped once per replay with
+ * hiccl_counter_add (one lane, stream-ordered: *ctr += v). */
+int hiccl_signal_wait_dev(uint32_t *const *sig, int nsig, const uint32_t *const *wait, int nwait,
+                          uint32_t epoch, const uint32_t *epoch_dev, uint32_t *err, double timeout_s,
+                          void *stream);
+int hiccl_counter_add(uint32_t *ctr, uint32_t v, void *stream);
 
 /* ----------------------------------------------------------------------
  * Measurement utilities (bench.py; not part of the reference surface).

@@ -28,10 +28,11 @@ HIP = os.path.join(ROOT, "build", "collectives_hip")
 HIP_F32 = os.path.join(ROOT, "build", "collectives_hip_f32")
 
 
-def mpirun(np_, exe, args, timeout=180, streamed=True, fused=False, engine="auto"):
+def mpirun(np_, exe, args, timeout=180, streamed=True, fused=False, engine="auto", graph=False, repeat=1):
     assert np_ <= 8
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED="1" if streamed else "0",
-               HICCL_FUSED_GATHER="1" if fused else "0", HICCL_SIGNAL_TIMEOUT="10", HICCL_ENGINE=engine)
+               HICCL_FUSED_GATHER="1" if fused else "0", HICCL_SIGNAL_TIMEOUT="10", HICCL_ENGINE=engine,
+               HICCL_GRAPH="1" if graph else "0", HICCL_DRIVER_REPEAT=str(repeat))
     cmd = ["timeout", "-k", "10", str(timeout), MPIRUN, "-np", str(np_), exe] + [str(a) for a in args]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd="/tmp")
     return p.returncode, p.stdout + p.stderr
@@ -66,18 +67,24 @@ def test_known_answer_fused_gather(np_, hier, libs, pattern, streamed):
     (8, 4099, 1, 1, 4, "1,4,2", "mpi,ipc,ipc"),
     (8, 4099, 1, 2, 2, "2,4", "ipc,ipc_get"),
 ])
-@pytest.mark.parametrize("streamed,fused,engine", [(True, False, "auto"), (False, False, "auto"),
-                                                   (True, True, "auto"), (False, True, "auto"),
-                                                   (False, False, "phase"), (True, True, "phase")],
-                         ids=["stream", "host", "stream-fused", "host-fused", "host-phase", "stream-fused-phase"])
+@pytest.mark.parametrize("streamed,fused,engine,graph", [
+    (True, False, "auto", False), (False, False, "auto", False), (True, True, "auto", False),
+    (False, True, "auto", False), (False, False, "phase", False), (True, True, "phase", False),
+    (True, False, "auto", True), (True, True, "auto", True)],
+    ids=["stream", "host", "stream-fused", "host-fused", "host-phase", "stream-fused-phase", "stream-graph",
+         "stream-fused-graph"])
 def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ring, depth, hier, libs, streamed,
-                                        fused, engine):
+                                        fused, engine, graph):
     """HICCL_ENGINE=phase forces the input-phased engine on every step's
-    batched plan (these shapes would pick the tile engine)."""
+    batched plan (these shapes would pick the tile engine).  Graph mode runs
+    the pipeline 4 times (eager, capture + replay, 2 replays) and checks the
+    last replay's bits."""
     prefix = str(tmp_path / "ar")
     rc, out = mpirun(np_, HIP_F32, [8, count, stripe, ring, depth, 0, 0, hier, libs, prefix], streamed=streamed,
-                     fused=fused, engine=engine)
+                     fused=fused, engine=engine, graph=graph, repeat=4 if graph else 1)
     assert rc == 0, out[-3000:]
+    if graph:
+        assert "graph replay" in out
     n = count * np_
     x = {r: oracle.fill(r + 1, n, 1234)[r] for r in range(np_)}
     libmap = {"mpi": S.MPI, "ipc": S.IPC, "ipc_get": S.IPC_GET, "xccl": S.XCCL}
@@ -94,6 +101,22 @@ def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ri
         got = np.fromfile(f"{prefix}.rank{r}.bin", dtype=np.float32)
         exp = mem[(r, ("recv",))]
         assert got.tobytes() == exp.tobytes(), f"rank {r}: {int((got != exp).sum())} differ"
+
+
+@pytest.mark.parametrize("np_,hier,libs", [(2, "2", "ipc"), (4, "2,2", "mpi,ipc"), (4, "4", "ipc_get")])
+@pytest.mark.parametrize("pattern", [4, 8])
+def test_known_answer_graph_replay(np_, hier, libs, pattern):
+    """HICCL_GRAPH=1 with measurement: Comm::measure's eager executions
+    advance the transports' epochs, so the next run() re-records the graph;
+    HiCCL::measure then replays it, and the reference's KAT validates the
+    final replay.  (Not 8 ranks: with 8 processes time-sharing the box's one
+    GPU, repeated stream-ordered runs stall past the signal timeout in eager
+    mode too -- DESIGN.md section 6; the 8-rank graph path is covered by
+    the float all-reduce test's 4 runs.)"""
+    rc, out = mpirun(np_, HIP, [pattern, 4099, 1, 1, 3, 1, 3, hier, libs], streamed=True, graph=True)
+    assert rc == 0, out[-3000:]
+    assert "PASSED!" in out
+    assert "graph replay" in out
 
 
 @pytest.mark.parametrize("streamed", [True, False], ids=["stream", "host"])
