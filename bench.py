@@ -143,6 +143,24 @@ def time_launches(fn, steps, warmup, dist=None):
     return t1 - t0, [a.elapsed_time(b) for a, b in evs]
 
 
+def time_queued(fn, steps, warmup):
+    """GPU time per launch with the stream kept busy: one event pair around
+    `steps` back-to-back launches, so host submission gaps are not counted
+    (small kernels: the per-launch event pairs of time_launches include the
+    time the GPU waits for the host to submit)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(steps):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / steps
+
+
 def mix_ceiling(ins, out, count, reps=10, mode=0):
     """Achievable HBM rate for this very access mix (n streams read + 1
     written, 16 B/lane, XOR instead of add; mode 1: the n reads only) from
@@ -669,12 +687,12 @@ def chunks(args):
                 comp.add([(t, off) for t in ins], (out, off), c, compid=0)
                 off += c
             stream = torch.cuda.current_stream()
-            res = {}
+            res, queued = {}, {}
             for mode in ("batched", "each"):
-                _, ms = time_launches(lambda: comp.start(stream=stream, each=(mode == "each")),
-                                      args.steps, args.warmup)
-                t = float(np.median(ms)) * 1e-3
-                res[mode] = t
+                launch = (lambda m=mode: comp.start(stream=stream, each=(m == "each")))
+                _, ms = time_launches(launch, args.steps, args.warmup)
+                res[mode] = float(np.median(ms)) * 1e-3
+                queued[mode] = time_queued(launch, max(args.steps, 20), 2) * 1e-3
             b = (n + 1) * count * esz
             ok = sample_check(out, n, count, bf16=(dtype == torch.bfloat16))
             print(json.dumps({"config": "C4", "dtype": str(dtype).split(".")[-1], "mib_per_input": mib,
@@ -682,7 +700,9 @@ def chunks(args):
                               "computes": depth, "batched_ms": round(res["batched"] * 1e3, 4),
                               "batched_GBps": round(b / res["batched"] / 1e9, 1),
                               "each_ms": round(res["each"] * 1e3, 4),
-                              "each_GBps": round(b / res["each"] / 1e9, 1)}), flush=True)
+                              "each_GBps": round(b / res["each"] / 1e9, 1),
+                              "queued_batched_GBps": round(b / queued["batched"] / 1e9, 1),
+                              "queued_each_GBps": round(b / queued["each"] / 1e9, 1)}), flush=True)
             comp.close()
             del ins, out
             torch.cuda.empty_cache()
