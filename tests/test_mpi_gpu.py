@@ -33,6 +33,12 @@ def mpirun(np_, exe, args, timeout=180, streamed=True, fused=False, engine="auto
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED="1" if streamed else "0",
                HICCL_FUSED_GATHER="1" if fused else "0", HICCL_SIGNAL_TIMEOUT="10", HICCL_ENGINE=engine,
                HICCL_GRAPH="1" if graph else "0", HICCL_DRIVER_REPEAT=str(repeat))
+    if np_ > 4:
+        # every rank on the box's one GPU: 8 processes x 4 hardware queues
+        # oversubscribe the device's queue slots, and a spinning stream-ordered
+        # wait can then outlast its timeout while the peer's queue is not
+        # mapped; 2 queues per process keep them all mapped
+        env["GPU_MAX_HW_QUEUES"] = "2"
     cmd = ["timeout", "-k", "10", str(timeout), MPIRUN, "-np", str(np_), exe] + [str(a) for a in args]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd="/tmp")
     return p.returncode, p.stdout + p.stderr
@@ -103,16 +109,14 @@ def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ri
         assert got.tobytes() == exp.tobytes(), f"rank {r}: {int((got != exp).sum())} differ"
 
 
-@pytest.mark.parametrize("np_,hier,libs", [(2, "2", "ipc"), (4, "2,2", "mpi,ipc"), (4, "4", "ipc_get")])
+@pytest.mark.parametrize("np_,hier,libs", [(2, "2", "ipc"), (4, "2,2", "mpi,ipc"), (4, "4", "ipc_get"),
+                                           (8, "1,4,2", "mpi,ipc,ipc")])
 @pytest.mark.parametrize("pattern", [4, 8])
 def test_known_answer_graph_replay(np_, hier, libs, pattern):
     """HICCL_GRAPH=1 with measurement: Comm::measure's eager executions
     advance the transports' epochs, so the next run() re-records the graph;
     HiCCL::measure then replays it, and the reference's KAT validates the
-    final replay.  (Not 8 ranks: with 8 processes time-sharing the box's one
-    GPU, repeated stream-ordered runs stall past the signal timeout in eager
-    mode too -- DESIGN.md section 6; the 8-rank graph path is covered by
-    the float all-reduce test's 4 runs.)"""
+    final replay."""
     rc, out = mpirun(np_, HIP, [pattern, 4099, 1, 1, 3, 1, 3, hier, libs], streamed=True, graph=True)
     assert rc == 0, out[-3000:]
     assert "PASSED!" in out
