@@ -406,6 +406,12 @@ def main():
     if dist.rank != 0:
         return 0
     props = torch.cuda.get_device_properties(0)
+    cus, mclk, bus = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    L.check(L.lib().hiccl_device_info(torch.cuda.current_device(), ctypes.byref(cus), ctypes.byref(mclk),
+                                      ctypes.byref(bus)), "device_info")
+    # HBM3E moves 4 bits per pin per reported memory clock (8 Gb/s per pin at
+    # the 2 GHz the runtime reports on MI355X): 8192 bits -> 8.19 TB/s, the spec
+    props_peak = 4.0 * mclk.value * 1e3 * bus.value / 8 / 1e9
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -437,6 +443,9 @@ def main():
         "cpu_baseline": cpu,
         "parity_sample_ok": parity,
         "device": props.name,
+        "device_props": {"gcn_arch": props.gcnArchName, "cus": cus.value, "mem_clock_khz": mclk.value,
+                         "mem_bus_width_bits": bus.value, "peak_GBps_from_props_x4": round(props_peak, 1),
+                         "total_mem_GiB": round(props.total_memory / 2**30, 1)},
         "control_plane": dist.backend,
     }
     print(json.dumps(line), flush=True)

@@ -93,6 +93,7 @@ _SIGS = {
     "hiccl_fill_uniform": (ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_size_t, ctypes.c_uint64,
                                           ctypes.c_uint32, ctypes.c_size_t, _vp]),
     "hiccl_stream_copy": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
+    "hiccl_device_info": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp]),
     "hiccl_signal_wait": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_uint32, _vp,
                                          ctypes.c_double, _vp]),
     "hiccl_signal_wait_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_uint32, _vp, _vp,

@@ -1607,6 +1607,26 @@ int hiccl_fill_uniform(int dtype, void *out, size_t count, uint64_t seed, uint32
   return check_hip(hipGetLastError(), "fill_uniform: launch");
 }
 
+int hiccl_device_info(int device, int *cus, int *mem_clock_khz, int *bus_width_bits) {
+  int v = 0;
+  if (cus) {
+    if (int e = check_hip(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device), "device_info: CUs"))
+      return e;
+    *cus = v;
+  }
+  if (mem_clock_khz) {
+    if (int e = check_hip(hipDeviceGetAttribute(&v, hipDeviceAttributeMemoryClockRate, device), "device_info: clock"))
+      return e;
+    *mem_clock_khz = v;
+  }
+  if (bus_width_bits) {
+    if (int e = check_hip(hipDeviceGetAttribute(&v, hipDeviceAttributeMemoryBusWidth, device), "device_info: bus"))
+      return e;
+    *bus_width_bits = v;
+  }
+  return 0;
+}
+
 int hiccl_stream_copy(void *dst, const void *src, size_t bytes, void *stream) {
   if (bytes == 0) return 0;
   if (!dst || !src) return fail(hipErrorInvalidValue, "stream_copy: NULL pointer");

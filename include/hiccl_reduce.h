@@ -247,6 +247,9 @@ int hiccl_counter_add(uint32_t *ctr, uint32_t v, void *stream);
 int hiccl_fill_uniform(int dtype, void *out, size_t count, uint64_t seed, uint32_t k,
                        size_t first, void *stream);
 int hiccl_stream_copy(void *dst, const void *src, size_t bytes, void *stream);
+/* hipDeviceProp values the roofline is checked against: CUs, peak memory
+ * clock (kHz) and memory bus width (bits); NULL outputs are skipped. */
+int hiccl_device_info(int device, int *cus, int *mem_clock_khz, int *bus_width_bits);
 
 #ifdef __cplusplus
 }
