@@ -97,3 +97,19 @@ def test_python_layer_refuses_cpu_tensors():
     x = torch.zeros(4)
     with pytest.raises(ValueError, match="device tensor"):
         hiccl_amd.reduce(x, [x])
+
+
+def test_header_is_c_and_plain_c_client_runs():
+    """include/hiccl_reduce.h compiles as C99 (-pedantic -Werror) and a C
+    client linked against the library passes its host-side checks."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        exe = os.path.join(d, "abi_c")
+        subprocess.run(["gcc", "-std=c99", "-pedantic", "-Wall", "-Wextra", "-Werror",
+                        "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "cpp", "abi_c.c"),
+                        "-o", exe, "-L", os.path.join(ROOT, "hiccl_amd"), "-lhiccl_reduce",
+                        "-Wl,-rpath," + os.path.join(ROOT, "hiccl_amd"), "-L/opt/rocm/lib", "-lamdhip64",
+                        "-Wl,-rpath,/opt/rocm/lib"], check=True)
+        p = subprocess.run([exe], capture_output=True, text=True)
+        assert p.returncode == 0 and "abi_c: PASSED" in p.stdout, p.stdout + p.stderr

@@ -567,3 +567,15 @@ def test_byte_copy_exact(nbytes):
     hiccl_amd.reduce_ptrs(L.HICCL_BYTES, g.data_ptr(), [f.data_ptr()], 16)
     torch.cuda.synchronize()
     assert g.view(torch.int32).tolist() == f.view(torch.int32).tolist()
+
+
+def test_plain_c_client_on_gpu():
+    """build/abi_c (tests/cpp/abi_c.c, built by make): a C99 program using
+    only include/hiccl_reduce.h reduces 3 device buffers, bit-exact with a
+    host loop in the reference's order."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "abi_c")
+    assert os.path.exists(exe), "run make"
+    p = subprocess.run(["timeout", "-k", "5", "60", exe, "gpu"], capture_output=True, text=True)
+    assert p.returncode == 0 and "abi_c: PASSED" in p.stdout, p.stdout + p.stderr
