@@ -112,9 +112,13 @@ def whole_job_gbps(world, bytes_per_step, steps, wall_max_s):
 # ----------------------------------------------------------- workloads -----
 
 def make_bucket(n, count, dtype=torch.float32, seed=SEED):
-    ins = [torch.empty(count, dtype=dtype, device="cuda") for _ in range(n)]
+    # integer buckets (size_t: the reference drivers' T) get the float
+    # generator's bits
+    fill_as = {torch.int64: torch.float64, torch.int32: torch.float32}.get(dtype, dtype)
+    ins = [torch.empty(count, dtype=fill_as, device="cuda") for _ in range(n)]
     for k, t in enumerate(ins):
         hiccl_amd.fill_uniform(t, seed, k)
+    ins = [t.view(dtype) for t in ins]
     out = torch.empty(count, dtype=dtype, device="cuda")
     torch.cuda.synchronize()
     return ins, out
@@ -623,8 +627,9 @@ def planvs(args):
 def crossover(args):
     """Engine crossover: one-shot reduce of n = 2/4/8 inputs, 1-512 MiB per
     input, f32 and bf16, TILE vs PHASE (sets the AUTO threshold)."""
-    dtypes = {"f32": (torch.float32,), "bf16": (torch.bfloat16,)}.get(args.xdtype,
-                                                                     (torch.float32, torch.bfloat16))
+    dtypes = {"f32": (torch.float32,), "bf16": (torch.bfloat16,), "f64": (torch.float64,), "u64": (torch.int64,),
+              "i32": (torch.int32,), "wide": (torch.float32, torch.float64, torch.int64, torch.int32)}.get(
+                  args.xdtype, (torch.float32, torch.bfloat16))
     mibs = [int(m) for m in args.xmib.split(",")] if args.xmib else (1, 4, 16, 32, 64, 128, 256, 512)
     ns = [int(m) for m in args.xn.split(",")] if args.xn else (2, 4, 8)
     for dtype in dtypes:

@@ -899,8 +899,12 @@ int auto_engine(uint64_t npkt, double n, int dtype, int acc, int dev) {
     if (tickets >= kTileMinTicketsPerWG * (uint64_t)device_cus(dev)) return HICCL_ENGINE_TILE;
   }
   const uint64_t chunk = (uint64_t)kPhBlock * phase_p_dtype(dtype, acc);
-  return npkt >= kPhaseMinChunksPerCU * (uint64_t)device_cus(dev) * chunk ? HICCL_ENGINE_PHASE
-                                                                          : HICCL_ENGINE_TILE;
+  const uint64_t per_cu = npkt / ((uint64_t)device_cus(dev) * chunk);  // phased chunks per CU
+  // two inputs: the static tile order leads from 2 to 16 chunks per CU (f32
+  // 64-512 MiB per input: +1-4 %), the phased order below and above it
+  // (32 MiB: 5.49 vs 5.17; 1 GiB: 6.13 vs 5.96 TB/s; r01g_xover_smalln.jsonl)
+  if (n < 2.5 && per_cu >= 2 && per_cu <= 16) return HICCL_ENGINE_TILE;
+  return per_cu >= kPhaseMinChunksPerCU ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
 }
 
 // Workgroups per CU: a tile launch too small for a phased chunk per CU has

@@ -383,13 +383,15 @@ def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
     """AUTO resolves to TILE with >= 5 inputs from 64 tickets per workgroup
     (n = 6: two tiles per ticket, 2^27 f32 per input on 256 CUs); otherwise
     to PHASE once every CU gets a chunk of 128 KiB (f32: 2^23 elements per
-    input), to TILE below."""
+    input), to TILE below -- and for two inputs also at 2-16 chunks per CU
+    (2^24-2^27 f32)."""
     count = 1 << 23
     a = torch.empty(1 << 27, device=DEV)
     hiccl_amd.fill_uniform(a, 77, 0)
     out = torch.empty(1 << 27, device=DEV)
     P, T = hiccl_amd.HICCL_ENGINE_PHASE, hiccl_amd.HICCL_ENGINE_TILE
-    for cnt, n, expect in ((1 << 27, 6, T), (1 << 26, 6, P), (count, 6, P), (count, 2, P), (count // 4, 6, T),
+    for cnt, n, expect in ((1 << 27, 6, T), (1 << 26, 6, P), (count, 6, P), (count, 2, P), (1 << 24, 2, T),
+                           (1 << 26, 4, P), (count // 4, 6, T),
                            (count // 4, 2, T)):
         comp = hiccl_amd.Compute(torch.float32, device=0)
         comp.add([a] * n, out, cnt, compid=0)
