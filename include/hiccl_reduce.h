@@ -56,7 +56,8 @@ typedef enum {
  *          added), then writes the chunk.
  *   AUTO   TILE (on the dynamic schedule, below) with >= 5 inputs once
  *          every workgroup gets >= 64 tickets (bf16: packed accumulator
- *          only); otherwise PHASE when every CU gets >= 1 chunk, else TILE
+ *          only); otherwise PHASE when every CU gets >= 1 chunk (two
+ *          inputs: not at 2-16 chunks per CU, where TILE leads), else TILE
  *          with 4 workgroups per CU (one-shot: that call; plan: all
  *          computes, packet-weighted mean n). */
 typedef enum {
