@@ -341,6 +341,7 @@ def main():
     ap.add_argument("--crossover", action="store_true")
     ap.add_argument("--planvs", action="store_true")
     ap.add_argument("--schedsweep", action="store_true")
+    ap.add_argument("--sweepdtype", default="f32", help="schedsweep: f32 | bf16")
     ap.add_argument("--sweepset", default="", help="schedsweep: '' (schedule/grab) | occupancy")
     ap.add_argument("--xdtype", default="both", help="crossover: f32 | bf16 | both")
     ap.add_argument("--xmib", default="", help="crossover: comma list of MiB per input")
@@ -561,6 +562,14 @@ def schedsweep(args):
                     ("t256x1_bpc4", dict(engine=1, unroll=1, blocks_per_cu=4)),
                     ("t256x4_dyn", dict(engine=1, schedule=2, grab=1)),
                     ("phase", dict(engine=2))]
+    if args.sweepset == "bf16occ":  # bf16 tile: hide the packed accumulator's VALU time
+        variants = [("auto", None),
+                    ("tile_dyn", dict(engine=1, schedule=2)),
+                    ("tile_dyn_bpc2", dict(engine=1, schedule=2, blocks_per_cu=2)),
+                    ("tile_dyn_bpc2_u2", dict(engine=1, schedule=2, blocks_per_cu=2, unroll=2)),
+                    ("tile_dyn_b512u2", dict(engine=1, schedule=2, block=512, unroll=2)),
+                    ("phase_static", dict(engine=2, schedule=1)),
+                    ("phase_bpc2", dict(engine=2, schedule=1, blocks_per_cu=2))]
     if args.sweepset == "xover":  # engine x schedule crossover (sets AUTO)
         variants = [("auto", None),
                     ("tile_dyn", dict(engine=1, schedule=2)),
@@ -569,8 +578,10 @@ def schedsweep(args):
                     ("phase_static", dict(engine=2, schedule=1)),
                     ("phase_dyn", dict(engine=2, schedule=2))]
     for n, mib in cases:
-        count = (mib << 20) // 4
-        ins, out = make_bucket(n, count)
+        sdt = torch.bfloat16 if args.sweepdtype == "bf16" else torch.float32
+        esz = 2 if sdt == torch.bfloat16 else 4
+        count = (mib << 20) // esz
+        ins, out = make_bucket(n, count, sdt)
         res = {}
         for rnd in range(5):
             for name, cfg in variants:
@@ -580,8 +591,9 @@ def schedsweep(args):
         row = {"mode": "schedsweep", "n": n, "mib_per_input": mib}
         for name, v in res.items():
             t = float(np.median(v)) * 1e-3
-            row[name] = round((n + 1) * count * 4 / t / 1e9, 1)
-        row["parity_sample_ok"] = sample_check(out, n, count)
+            row[name] = round((n + 1) * count * esz / t / 1e9, 1)
+        row["dtype"] = str(sdt).split(".")[-1]
+        row["parity_sample_ok"] = sample_check(out, n, count, bf16=(sdt == torch.bfloat16))
         print(json.dumps(row), flush=True)
         del ins, out
         torch.cuda.empty_cache()
