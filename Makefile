@@ -22,7 +22,8 @@ LIBFLAGS = -mllvm -amdgpu-atomic-optimizer-strategy=None
 $(LIB): hiccl_amd/csrc/reduce.hip include/hiccl_reduce.h
 	$(HIPCC) $(HIPFLAGS) $(LIBFLAGS) -o $@ $<
 
-oracle:
+# oracle/_ref/collectives_main_hip links the HIP library: build it first
+oracle: $(LIB)
 	$(MAKE) -C oracle
 
 clean:
@@ -37,8 +38,10 @@ MPI_LIB ?= /opt/conda/lib
 CXX ?= g++
 CXXFLAGS = -std=c++17 -O2 -Wall -Wno-unused-function -Iinclude -I$(MPI_INC)
 MPI_LINK = $(MPI_LIB)/libmpi.so -Wl,-rpath,/usr/lib/x86_64-linux-gnu:$(MPI_LIB)
-HIP_HOST = -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
-HIP_LINK = -Lhiccl_amd -lhiccl_reduce -Wl,-rpath,'$$ORIGIN/../hiccl_amd' -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+# the XCCL level runs on RCCL point-to-point (include/hiccl/transport.h)
+HIP_HOST = -D__HIP_PLATFORM_AMD__ -DHICCL_WITH_RCCL -I/opt/rocm/include
+HIP_LINK = -Lhiccl_amd -lhiccl_reduce -Wl,-rpath,'$$ORIGIN/../hiccl_amd' -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib
+ABI_LINK = -Lhiccl_amd -lhiccl_reduce -Wl,-rpath,'$$ORIGIN/../hiccl_amd' -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
 HDRS = include/hiccl.h $(wildcard include/hiccl/*.h) include/hiccl_reduce.h hiccl_amd/csrc/compose.h
 
 CPP_BINS = build/plan_dump build/collectives_host build/collectives_host_f32 build/collectives_hip build/collectives_hip_f32 \
@@ -77,6 +80,6 @@ build/readme_example_hip: hiccl_amd/csrc/readme_example.cpp $(HDRS) $(LIB)
 # plain C99 client of the C ABI (the header must stay C)
 build/abi_c: tests/cpp/abi_c.c include/hiccl_reduce.h $(LIB)
 	@mkdir -p build
-	gcc -std=c99 -pedantic -Wall -Wextra -Werror -Iinclude -o $@ $< $(HIP_LINK)
+	gcc -std=c99 -pedantic -Wall -Wextra -Werror -Iinclude -o $@ $< $(ABI_LINK)
 
 .PHONY: cpp

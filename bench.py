@@ -5,7 +5,7 @@ Default workload = BASELINE config 2: N = 8 inputs x 2^28 fp32 (1 GiB each)
 -> one 1 GiB output, device-resident.  One "step" = one hiccl_reduce launch
 over the whole bucket.  value = whole-job GB/s = world_size x (N+1) x count x
 4 B x steps / max-over-ranks wall time (the reference's own byte accounting,
-source/compute.h:251-257).  Multi-GPU: every rank reduces its own bucket
+source/compute.h:197-203).  Multi-GPU: every rank reduces its own bucket
 (replicas, weak scaling -- the stage is per-GPU local).
 
 Extra objects on the JSON line:
@@ -29,6 +29,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -53,6 +54,12 @@ def log(*a):
 # ----------------------------------------------------------------- dist ----
 
 class Dist:
+    """One process per GPU (torchrun env).  The control plane -- the barrier
+    around the timed region and the max-over-ranks time -- is gloo on the
+    host: it is started before any GPU is touched (the config-5 leg runs an
+    MPI job on every GPU first) and there is no data-path collective (the
+    stage is per-GPU local)."""
+
     def __init__(self, gpus):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
@@ -63,44 +70,102 @@ class Dist:
                 self.world = 1
             else:
                 log(f"bench: WORLD_SIZE={self.world} but --gpus {gpus}")
+        self.pg = init_control_plane() if self.world > 1 else None
+        self.backend = "gloo" if self.pg else None
         ndev = torch.cuda.device_count()
         self.device = self.local % max(ndev, 1)
         if ndev:  # (no device: only the control plane, as in tests/test_bench_dist.py)
             torch.cuda.set_device(self.device)
-        self.pg = None
-        self.backend = None
-        if self.world > 1:
-            import torch.distributed as dist
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            # RCCL when every rank owns a GPU; gloo when ranks share one (a
-            # rehearsal on a 1-GPU box).  Either way only the barrier and the
-            # max-over-ranks time cross ranks: no data-path collective.
-            if self.world <= ndev:
-                self.backend = "nccl"
-                dist.init_process_group("nccl", device_id=torch.device("cuda", self.device))
-            else:
-                self.backend = "gloo"
-                dist.init_process_group("gloo")
-            self.pg = dist
 
     def barrier(self):
         if self.pg:
-            if self.backend == "nccl":
-                self.pg.barrier(device_ids=[self.device])
-            else:
-                self.pg.barrier()
+            self.pg.barrier()
 
     def max(self, x):
         if not self.pg:
             return x
-        dev = "cuda" if self.backend == "nccl" else "cpu"
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64)
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
 
     def close(self):
         if self.pg:
             self.pg.destroy_process_group()
+
+
+def init_control_plane():
+    """The gloo process group over the torchrun ranks (CPU only)."""
+    import torch.distributed as tdist
+    if not tdist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        tdist.init_process_group("gloo")
+    return tdist
+
+
+# ------------------------------------------------------------ config 5 -----
+
+C5_EXE = os.path.join(ROOT, "build", "collectives_hip_f32")
+
+
+def c5_leg(args):
+    """Config 5 in situ (collectives/main.cpp:151-155): the all-reduce
+    composition (reduce-scatter + fence + all-gather) over every GPU of the
+    job, hierarchy {1, N/2, 2} = {1,4,2} at N = 8 with {MPI, IPC, IPC},
+    pipedepth 128, 2^25 floats per rank per chunk (a 1 GiB send buffer per
+    rank at 8 ranks), this build's C++ Comm<float> with the HIP reduction
+    stage -- run by rank 0 as an MPI job (one rank per GPU) BEFORE any torch
+    rank touches a GPU; the other ranks wait on the gloo control plane.
+    Returns the job's JSON (per mode) or why it was skipped; never the bench
+    `value`."""
+    tdist = init_control_plane()
+    res = None
+    if tdist.get_rank() == 0:
+        try:
+            res = run_c5(tdist.get_world_size(), args)
+        except Exception as e:  # the leg must not cost the headline line
+            res = {"skipped": f"error: {e}"}
+    obj = [res]
+    tdist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def run_c5(world, args):
+    import shutil
+    import tempfile
+    ndev = torch.cuda.device_count()  # (does not initialise HIP)
+    if ndev < world:
+        return {"skipped": f"{world} ranks on {ndev} GPU(s): config 5 needs one GPU per rank"}
+    if not os.path.exists(C5_EXE):
+        return {"skipped": f"{C5_EXE} not built"}
+    mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
+    hier = f"1,{world // 2},2" if world % 2 == 0 and world >= 4 else str(world)
+    libs = "mpi,ipc,ipc" if hier.count(",") == 2 else "ipc"
+    count = 1 << args.c5_log2count
+    out = {"workload": f"C5: all-reduce of {count * world * 4 >> 20} MiB fp32 per rank, {world} ranks, hierarchy "
+                       f"{{{hier}}} {{{libs}}}, pipedepth 128 (collectives/main.cpp:151-155)"}
+    modes = (("host", {"HICCL_STREAM_ORDERED": "0"}),
+             ("stream_graph_fused", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "1"}))
+    for name, extra in modes:
+        fd, path = tempfile.mkstemp(prefix="hiccl_c5_", suffix=".json", dir="/tmp")
+        os.close(fd)
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_DRIVER_JSON=path, OMP_NUM_THREADS="1",
+                   HICCL_SIGNAL_TIMEOUT="30", **extra)
+        cmd = ["timeout", "-k", "10", "300", mpirun, "-np", str(world), C5_EXE, "8", str(count), "1", "1", "128",
+               "2", str(args.c5_iters), hier, libs]
+        t0 = time.perf_counter()
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, cwd="/tmp")
+        try:
+            r = json.load(open(path))
+        except (OSError, ValueError):
+            r = {"error": f"rc {p.returncode}: {(p.stdout + p.stderr)[-600:]}"}
+        finally:
+            os.unlink(path)
+        r["wall_s"] = round(time.perf_counter() - t0, 1)
+        out[name] = r
+        log(f"bench: c5 {name}: {r}")
+        if p.returncode not in (0, 1):
+            break  # a crash or a time-out: start nothing more on the GPUs
+    return out
 
 
 def whole_job_gbps(world, bytes_per_step, steps, wall_max_s):
@@ -201,34 +266,99 @@ def copy_ceiling(nbytes=1 << 30, reps=10):
 
 # --------------------------------------------------------- CPU baseline ----
 
-def cpu_baseline(n, count, budget_s=10.0):
-    """The reference's CPU reduce_kernel (or the restatement) on this host.
+def host_cpus():
+    """CPUs this process may use: the affinity set, capped by a cgroup CPU
+    quota (a GPU box slice), and the physical cores among them."""
+    aff = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    cores = set()
+    for c in aff:
+        try:
+            pkg = open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id").read().strip()
+            core = open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id").read().strip()
+            cores.add((pkg, core))
+        except OSError:
+            cores.add(("?", str(c)))
+    threads = min(len(aff), quota) if quota else len(aff)
+    return {"threads": threads, "affinity_cpus": len(aff), "cgroup_quota_cpus": quota,
+            "physical_cores_in_affinity": len(cores)}
 
-    Sample: the full config-2 bucket (n x count fp32), first-touch-initialised
-    in parallel by the oracle generator, reduced repeatedly until ~budget_s
-    of CPU work; reports the median pass."""
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
+
+
+def cpu_baseline(n, count, budget_s=10.0, gpu_out=None):
+    """The reference's CPU reduce_kernel on this host, in a child process so
+    OpenMP starts with OMP_NUM_THREADS = every CPU this process may use and
+    OMP_PROC_BIND=spread (libgomp reads them once, at load; BASELINE.md:34).
+    `gpu_out`: the GPU's output of the same bucket (a host float32 array):
+    the child compares all `count` words with the reference's own output
+    (the full-bucket parity check)."""
+    cpus = host_cpus()
+    env = dict(os.environ, OMP_NUM_THREADS=str(cpus["threads"]), OMP_PROC_BIND="spread", OMP_PLACES="cores"
+               if cpus["physical_cores_in_affinity"] >= cpus["threads"] else "threads")
+    path = None
+    if gpu_out is not None:
+        import tempfile
+        fd, path = tempfile.mkstemp(prefix="hiccl_gpu_out_", suffix=".f32", dir="/tmp")
+        with os.fdopen(fd, "wb") as fh:
+            gpu_out.tofile(fh)
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-leg", "--n", str(n), "--log2count",
+           str(int(np.log2(count))), "--cpu-budget", str(budget_s)]
+    if path:
+        cmd += ["--expect-file", path]
+    try:
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=max(120.0, 6 * budget_s))
+    finally:
+        if path:
+            os.unlink(path)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        log("bench: cpu leg failed:", p.returncode, p.stderr[-2000:])
+        return None, None
+    res = json.loads(lines[-1])
+    parity = res.pop("parity_full", None)
+    res["cores"] = res.pop("threads")
+    res.update({k: v for k, v in cpus.items() if k != "threads"})
+    return res, parity
+
+
+def cpu_leg(args):
+    """Child of cpu_baseline(): time the reference reduce_kernel (or the C
+    restatement) over the full bucket; optionally compare with a GPU output."""
+    n, count = args.n, 1 << args.log2count
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libhiccl_ref.so")
-    ora_so = os.path.join(ROOT, "oracle", "liboracle.so")
-    if not os.path.exists(ora_so):
-        return None
-    ora = ctypes.CDLL(ora_so)
+    ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
     ora.oracle_num_threads.restype = ctypes.c_int
-    threads = ora.oracle_num_threads()
     if os.path.exists(ref_so):
         lib, kind = ctypes.CDLL(ref_so), "reference"
         fn = lib.ref_reduce_f32
         fn.restype = None
         fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int]
     else:
-        lib, kind = ora, "port"
+        kind = "port"
         fn = ora.oracle_reduce_f32
         fn.restype = None
         fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+    threads = ora.oracle_num_threads()
     fill = ora.oracle_fill_uniform_f32
     fill.restype = None
     fill.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t]
     bufs = [np.empty(count, np.float32) for _ in range(n)]
-    for k, b in enumerate(bufs):
+    for k, b in enumerate(bufs):  # parallel first touch inside the generator
         fill(b.ctypes.data, count, SEED, k, 0)
     out = np.empty(count, np.float32)
     fill(out.ctypes.data, count, SEED, 99, 0)  # first touch of the output
@@ -245,31 +375,21 @@ def cpu_baseline(n, count, budget_s=10.0):
     one()  # warm
     times = []
     t_start = time.perf_counter()
-    while time.perf_counter() - t_start < budget_s and len(times) < 50:
+    while time.perf_counter() - t_start < args.cpu_budget and len(times) < 50:
         times.append(one())
     med = float(np.median(times))
-    # spot-check the CPU result against the generator at a few indices
-    idx = np.array([0, 1, count // 2, count - 1], np.uint64)
-    chk = np.empty(4, np.float32)
-    ss = ora.oracle_sample_sum_f32
-    ss.restype = None
-    ss.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int]
-    ss(chk.ctypes.data, idx.ctypes.data, 4, SEED, n)
-    assert np.array_equal(chk.view(np.uint32), out[idx.astype(np.int64)].view(np.uint32))
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    gbps = (n + 1) * count * 4 / med / 1e9
-    del bufs, out
-    return {"value": round(gbps, 2), "unit": "GB/s", "cores": threads, "kind": kind,
-            "sample": f"{n} x 2^{int(np.log2(count))} fp32 -> 1 output (the full config-2 bucket), "
-                      f"median of {len(times)} passes ({med * 1e3:.1f} ms each), "
-                      f"OpenMP {threads} threads, {cpu_model}"}
+    res = {"value": round((n + 1) * count * 4 / med / 1e9, 2), "unit": "GB/s", "threads": threads, "kind": kind,
+           "sample": f"{n} x 2^{args.log2count} fp32 -> 1 output (the full config-2 bucket), median of "
+                     f"{len(times)} passes ({med * 1e3:.1f} ms each), OpenMP {threads} threads "
+                     f"(OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND', '')}), {cpu_model()}"}
+    if args.expect_file:
+        got = np.fromfile(args.expect_file, dtype=np.float32)
+        ok = got.size == count
+        bad = int(np.count_nonzero(got.view(np.uint32) != out.view(np.uint32))) if ok else count
+        res["parity_full"] = {"ok": ok and bad == 0, "mismatches": bad, "words": count,
+                              "against": f"{kind} reduce_kernel (compute.h:14-23) on the same generator and seed"}
+    print(json.dumps(res), flush=True)
+    return 0
 
 
 def sample_check(out, n, count, bf16=False, seed=SEED, nsample=1024):
@@ -347,8 +467,20 @@ def main():
     ap.add_argument("--xmib", default="", help="crossover: comma list of MiB per input")
     ap.add_argument("--xn", default="", help="crossover: comma list of input counts")
     ap.add_argument("--buckets", type=int, default=0, help="schedsweep: this many fresh --n x 2^--log2count buckets")
+    ap.add_argument("--cpu-leg", action="store_true", help=argparse.SUPPRESS)  # child of cpu_baseline()
+    ap.add_argument("--expect-file", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--no-c5", action="store_true", help="N > 1: skip the config-5 all-reduce leg")
+    ap.add_argument("--c5-log2count", type=int, default=25,
+                    help="config-5 leg: elements per rank per chunk = 2^x (25: 1 GiB fp32 send buffer at 8 ranks)")
+    ap.add_argument("--c5-iters", type=int, default=5)
     args = ap.parse_args()
+    if args.cpu_leg:
+        return cpu_leg(args)
 
+    c5 = None
+    if os.environ.get("WORLD_SIZE", "1") != "1" and not args.no_c5:
+        # before this process touches a GPU: the MPI job owns every GPU meanwhile
+        c5 = c5_leg(args)
     dist = Dist(args.gpus)
     if args.sweep:
         return sweep(args)
@@ -382,6 +514,12 @@ def main():
     kern_s = float(np.mean(kms)) * 1e-3
     achieved = bytes_step / kern_s / 1e9
 
+    # full-bucket parity (N = 1, rank 0): the GPU's whole output against the
+    # reference's own CPU reduce_kernel on the same generator and seed, done
+    # by the CPU baseline leg below
+    gpu_out = None
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu and cfg is None:
+        gpu_out = out.cpu().numpy()
     # parity spot check of this very output against the oracle generator
     parity = None
     ora_so = os.path.join(ROOT, "oracle", "liboracle.so")
@@ -404,9 +542,12 @@ def main():
     parity = bool(dist.max(0.0 if parity in (True, None) else 1.0) == 0.0) if parity is not None else None
     copy_gbps = copy_ceiling() if dist.rank == 0 else None
     prof = traffic_from_profiles(n, count) if cfg is None else None
-    cpu = None
+    cpu, parity_full = None, None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(n, count, args.cpu_budget)
+        cpu, parity_full = cpu_baseline(n, count, args.cpu_budget, gpu_out)
+        if parity_full and not parity_full["ok"]:
+            log(f"bench: FULL-BUCKET PARITY FAILURE: {parity_full['mismatches']} of {count} words differ")
+    del gpu_out
     dist.close()
     if dist.rank != 0:
         return 0
@@ -436,6 +577,9 @@ def main():
                    "kernel_config": cfg or "default", "parallelism": f"replicas x{dist.world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     # the HBM-read view: the n input reads only
+                     "read_achieved_GBps": round(n * count * 4 / kern_s / 1e9, 1),
+                     "read_frac": round(n * count * 4 / kern_s / 1e9 / HBM_PEAK_GBPS, 4),
                      "traffic": (prof or {}).get("hbm_bytes_per_launch"),
                      "kernel_ms_mean": round(kern_s * 1e3, 4), "kernel_ms_min": round(min(kms), 4),
                      "mix_ceiling_GBps": round(mix_gbps, 1) if mix_gbps else None,
@@ -446,6 +590,7 @@ def main():
                      "frac_of_copy": round(achieved / copy_gbps, 4) if copy_gbps else None,
                      "traffic_source": (prof or {}).get("source")},
         "cpu_baseline": cpu,
+        "parity_full": parity_full,
         "parity_sample_ok": parity,
         "device": props.name,
         "device_props": {"gcn_arch": props.gcnArchName, "cus": cus.value, "mem_clock_khz": mclk.value,
@@ -453,6 +598,8 @@ def main():
                          "total_mem_GiB": round(props.total_memory / 2**30, 1)},
         "control_plane": dist.backend,
     }
+    if c5 is not None:
+        line["c5"] = c5
     print(json.dumps(line), flush=True)
     return 0
 
@@ -694,7 +841,7 @@ def c2variants(args):
 def chunks(args):
     """Config 4: fp32/bf16, 16 MiB..4 GiB per input, split into 1 MiB computes
     (pipedepth = bytes / 1 MiB, reduce.h:406 split), batched plan launch vs
-    one launch per compute (the reference structure, compute.h:141-145)."""
+    one launch per compute (the reference structure, compute.h:88-91)."""
     n = 8
     for dtype in (torch.float32, torch.bfloat16):
         esz = torch.tensor([], dtype=dtype).element_size()

@@ -77,6 +77,7 @@ _SIGS = {
     "hiccl_reduce_plan_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int]),
     "hiccl_reduce_plan_set_acc": (ctypes.c_int, [_vp, ctypes.c_int]),
     "hiccl_reduce_plan_set_engine": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "hiccl_reduce_plan_set_config": (ctypes.c_int, [_vp, ctypes.POINTER(ReduceConfig)]),
     "hiccl_reduce_plan_engine": (ctypes.c_int, [_vp]),
     "hiccl_reduce_plan_add": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_size_t]),
     "hiccl_reduce_plan_launch": (ctypes.c_int, [_vp, _vp]),

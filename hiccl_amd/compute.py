@@ -1,7 +1,7 @@
 """Python mirror of the reference's reduction compute stage.
 
-``reduce`` is one registered compute launched once (source/compute.h:145);
-``Compute`` mirrors ``HiCCL::Compute<T>`` (source/compute.h:80-258):
+``reduce`` is one registered compute launched once (source/compute.h:90-91);
+``Compute`` mirrors ``HiCCL::Compute<T>`` (source/compute.h:26-204):
 ``add`` / ``start`` / ``wait`` / ``report`` / ``measure`` with the same
 argument meaning.  Both call straight into the HIP library through the C ABI
 (include/hiccl_reduce.h); device memory and streams come from torch.
@@ -92,20 +92,20 @@ def reduce_ptrs(dtype_code, out_ptr, in_ptrs, count, stream=None, config=None):
 
 
 class Compute:
-    """``HiCCL::Compute<T>`` (source/compute.h:80-258) on the batched plan.
+    """``HiCCL::Compute<T>`` (source/compute.h:26-204) on the batched plan.
 
-    add(inputbuf, outputbuf, count, compid)  compute.h:101-139 -- records the
+    add(inputbuf, outputbuf, count, compid)  compute.h:47-85 -- records the
         compute only when ``myid == compid`` (SPMD: every rank calls add).
         ``inputbuf`` is a list of tensors or (tensor, element_offset) pairs,
         ``outputbuf`` a tensor or (tensor, element_offset).
-    start()   compute.h:141-160 -- ONE batched kernel for all computes.
-    wait()    compute.h:161-171.
-    report()  compute.h:173-189 (local numbers; the Comm layer gathers).
-    measure(warmup, numiter[, count])  compute.h:191-257.
+    start()   compute.h:87-106 -- ONE batched kernel for all computes.
+    wait()    compute.h:107-117.
+    report()  compute.h:119-135 (local numbers; the Comm layer gathers).
+    measure(warmup, numiter[, count])  compute.h:137-203.
     """
 
     def __init__(self, dtype=torch.float32, device=None, myid=0, acc=L.HICCL_ACC_NATIVE,
-                 engine=L.HICCL_ENGINE_AUTO):
+                 engine=L.HICCL_ENGINE_AUTO, config=None):
         self.dtype = dtype
         self.code = L.DTYPE_OF_TORCH[dtype]
         if device is None:
@@ -124,6 +124,15 @@ class Compute:
             L.check(L.lib().hiccl_reduce_plan_set_acc(self._plan, acc), "plan_set_acc")
         if engine != L.HICCL_ENGINE_AUTO:
             L.check(L.lib().hiccl_reduce_plan_set_engine(self._plan, engine), "plan_set_engine")
+        if config is not None:
+            self.set_config(config)
+
+    def set_config(self, config):
+        """Kernel configuration of the plan (dict of hiccl_reduce_config_t
+        fields; hiccl_reduce_plan_set_config).  A field the plan kernels do
+        not honour raises HicclError."""
+        cfg = L.ReduceConfig(**config)
+        L.check(L.lib().hiccl_reduce_plan_set_config(self._plan, ctypes.byref(cfg)), "plan_set_config")
 
     def engine(self):
         """Engine the last upload resolved to (HICCL_ENGINE_TILE / _PHASE)."""
@@ -158,8 +167,15 @@ class Compute:
 
     def start(self, stream=None, each=False):
         """Launch on ``stream`` (torch stream or raw handle); default = the
-        plan's own stream (the reference keeps one per compute, compute.h:131)."""
-        s = _stream_handle(stream) if stream is not None else ctypes.c_void_p(self.stream_handle())
+        plan's own stream (the reference keeps one per compute, compute.h:76-78),
+        ordered after the work already queued on torch's current stream (the
+        inputs it produced), so no synchronisation is needed first."""
+        if stream is None:
+            own = torch.cuda.ExternalStream(self.stream_handle(), device=self.device)
+            own.wait_stream(torch.cuda.current_stream(self.device))
+            s = ctypes.c_void_p(self.stream_handle())
+        else:
+            s = _stream_handle(stream)
         fn = L.lib().hiccl_reduce_plan_launch_each if each else L.lib().hiccl_reduce_plan_launch
         L.check(fn(self._plan, s), "plan_launch")
 
@@ -167,7 +183,7 @@ class Compute:
         L.check(L.lib().hiccl_reduce_plan_sync(self._plan), "plan_sync")
 
     def bytes(self):
-        """Sum of count * (n + 1) * sizeof(T) (compute.h:251-257)."""
+        """Sum of count * (n + 1) * sizeof(T) (compute.h:197-203)."""
         return L.lib().hiccl_reduce_plan_bytes(self._plan)
 
     def report(self):
@@ -175,11 +191,11 @@ class Compute:
         return f"numcomp: {self.numcomp}({numinput})"
 
     def measure(self, warmup, numiter, count=None, each=False):
-        """Time start()+wait() like compute.h:191-250; returns the stats dict.
+        """Time start()+wait() like compute.h:137-196; returns the stats dict.
 
         ``count`` is the element count the GB/s figure is priced on
-        (compute.h:242); default = the two-argument overload's
-        sum of count*(n+1) (compute.h:251-257), i.e. reads + writes.
+        (compute.h:188); default = the two-argument overload's
+        sum of count*(n+1) (compute.h:197-203), i.e. reads + writes.
         """
         import time
         data = (self.bytes() if count is None else count * torch.tensor([], dtype=self.dtype).element_size())

@@ -18,6 +18,7 @@
 // float with -DHICCL_DRIVER_FLOAT.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -70,6 +71,75 @@ static inline uint64_t splitmix64(uint64_t z) {
 static inline float uniform_f32(uint64_t seed, uint32_t k, uint64_t i) {
   uint64_t h = splitmix64(splitmix64(seed ^ ((uint64_t)k << 48)) + i);
   return (float)(uint32_t)(h >> 40) * (1.0f / 8388608.0f) - 1.0f;
+}
+
+// HICCL_DRIVER_JSON=<path> (rank 0 writes it): HiCCL::measure of the whole
+// collective (bench.h:2-60 semantics: barrier, run, MAX over ranks), the
+// per-step kernel time of each rank's batched compute (HIP events; MAX over
+// ranks of the per-run total), and, for all-reduce, a known-answer check
+// that is exact in any float type: sendbuf[i] = (i mod 1021) - 510 on every
+// rank, so every partial sum is a small integer and recvbuf[i] must equal
+// numproc * sendbuf[i] whatever the summation order.
+static int bench_json(const char *path, HiCCL::Comm<Type> &coll, Type *sendbuf_d, Type *recvbuf_d, size_t count,
+                      int pattern, int warmup, int numiter, const std::vector<int> &hierarchy,
+                      const std::vector<CommBench::library> &libs, int pipedepth) {
+  const int myid = CommBench::myid, numproc = CommBench::numproc;
+  const size_t n = count * numproc;
+  std::vector<Type> host(n);
+  for (size_t i = 0; i < n; i++) host[i] = (Type)((double)(i % 1021) - 510.0);
+  CommBench::memcpyH2D(sendbuf_d, host.data(), n);
+  double kern_ms = 0, kern_bytes = 0;
+  int ksteps = 0;
+#ifndef HICCL_PORT_HOST
+  for (auto &kt : coll.compute_kernel_times(5)) {
+    kern_ms += kt.first;
+    kern_bytes += (double)kt.second;
+    ksteps++;
+  }
+#endif
+  double kmax[2] = {kern_ms, kern_bytes};
+  MPI_Allreduce(MPI_IN_PLACE, kmax, 2, MPI_DOUBLE, MPI_MAX, CommBench::comm_mpi);
+  HiCCL::Times t = HiCCL::measure<Type>(warmup, numiter, n, coll);
+  // known-answer check on the same inputs (the measure runs left recvbuf
+  // holding the all-reduce of sendbuf)
+  {
+    std::vector<Type> fill(n);
+    std::memset((void *)fill.data(), 0xff, n * sizeof(Type));
+    CommBench::memcpyH2D(recvbuf_d, fill.data(), n);
+  }
+  MPI_Barrier(CommBench::comm_mpi);
+  coll.run();
+  std::vector<Type> out(n);
+  CommBench::memcpyD2H(out.data(), recvbuf_d, n);
+  size_t bad = 0;
+  if (pattern == HiCCL::allreduce)
+    for (size_t i = 0; i < n; i++)
+      if (out[i] != (Type)(numproc * ((double)(i % 1021) - 510.0))) bad++;
+  unsigned long tot = bad;
+  MPI_Allreduce(MPI_IN_PLACE, &tot, 1, MPI_UNSIGNED_LONG, MPI_SUM, CommBench::comm_mpi);
+  if (myid == 0) {
+    std::string h, l;
+    for (size_t i = 0; i < hierarchy.size(); i++) h += (i ? "," : "") + std::to_string(hierarchy[i]);
+    for (size_t i = 0; i < libs.size(); i++) l += std::string(i ? "," : "") + CommBench::lib_name(libs[i]);
+    FILE *f = std::fopen(path, "w");
+    if (!f) CommBench::die("HICCL_DRIVER_JSON", path);
+    const double data = (double)n * sizeof(Type);
+    std::fprintf(f,
+                 "{\"ranks\": %d, \"pattern\": %d, \"hierarchy\": \"%s\", \"libs\": \"%s\", \"pipedepth\": %d, "
+                 "\"count_per_rank_chunk\": %zu, \"sendbuf_bytes_per_rank\": %.0f, \"mode\": \"%s%s%s\", "
+                 "\"iterations\": %zu, \"collective_ms_min\": %.4f, \"collective_ms_median\": %.4f, "
+                 "\"collective_ms_max\": %.4f, \"algorithmic_GBps_median\": %.2f, "
+                 "\"kernel_steps_rank0\": %d, \"kernel_ms_per_run_max_rank\": %.4f, "
+                 "\"kernel_us_per_step_rank0\": %.3f, \"kernel_GBps_max_rank\": %.1f, "
+                 "\"kat_exact_mismatches\": %lu, \"kat\": \"%s\"}\n",
+                 numproc, pattern, h.c_str(), l.c_str(), pipedepth, count, data, coll.stream_ordered() ? "stream-ordered" : "host-driven",
+                 coll.graph_mode() ? "+graph" : "", coll.fused_gather() ? "+fused" : "", t.t.size(), t.min() * 1e3,
+                 t.median() * 1e3, t.max() * 1e3, t.median() > 0 ? data / t.median() / 1e9 : 0.0, ksteps, kmax[0],
+                 ksteps ? kern_ms / ksteps * 1e3 : 0.0, kmax[0] > 0 ? kmax[1] / (kmax[0] * 1e-3) / 1e9 : 0.0, tot,
+                 pattern != HiCCL::allreduce ? "n/a" : tot == 0 ? "PASSED" : "FAILED");
+    std::fclose(f);
+  }
+  return tot == 0 ? 0 : 1;
 }
 
 int main(int argc, char *argv[]) {
@@ -142,11 +212,18 @@ int main(int argc, char *argv[]) {
       if (!f || std::fwrite(out.data(), sizeof(Type), out.size(), f) != out.size()) CommBench::die("dump", path);
       std::fclose(f);
     }
-    if (numiter > 0) {
-      coll.measure(warmup, numiter, count * numproc / pipedepth);
-      HiCCL::measure<Type>(warmup, numiter, count * numproc, coll);
+    const char *json = std::getenv("HICCL_DRIVER_JSON");
+    if (json && numiter > 0) {
+      // bench.py's config-5 leg: whole-collective times, per-step kernel
+      // times, and a float-exact known-answer check, as one JSON object
+      rc = bench_json(json, coll, sendbuf_d, recvbuf_d, count, pattern, warmup, numiter, hierarchy, libs, pipedepth);
+    } else {
+      if (numiter > 0) {
+        coll.measure(warmup, numiter, count * numproc / pipedepth);
+        HiCCL::measure<Type>(warmup, numiter, count * numproc, coll);
+      }
+      if (!dump || sizeof(Type) == 8) rc = HiCCL::validate(sendbuf_d, recvbuf_d, count, pattern, root, coll) ? 0 : 1;
     }
-    if (!dump || sizeof(Type) == 8) rc = HiCCL::validate(sendbuf_d, recvbuf_d, count, pattern, root, coll) ? 0 : 1;
   }
   CommBench::free(sendbuf_d);
   CommBench::free(recvbuf_d);

@@ -40,7 +40,7 @@ bool compose(Sink &s, int pattern, T *sendbuf, T *recvbuf, size_t count, int np,
     case reducescatter:
       for (int p = 0; p < np; p++) s.reduce(sendbuf, p * count, recvbuf, 0, count, ids(np, np, p), p);
       return true;
-    case allreduce:  // reduce-scatter + fence + all-gather (collectives/main.cpp:378-383)
+    case allreduce:  // reduce-scatter + fence + all-gather (collectives/main.cpp:151-155)
       for (int p = 0; p < np; p++) s.reduce(sendbuf, p * count, recvbuf, p * count, count, ids(np, np, p), p);
       s.fence();
       for (int p = 0; p < np; p++) s.bcast(recvbuf, p * count, recvbuf, p * count, count, p, ids(-1, np, p));

@@ -19,13 +19,13 @@
 //  * two engines: TILE (all n inputs of a 16 KiB tile loaded together) and
 //    PHASE (a 128 KiB chunk swept input by input); AUTO picks per launch;
 //  * the input pointer table travels in the kernarg segment (scalar loads,
-//    no device-side T** table and no H2D copy per call, cf. compute.h:124-126);
+//    no device-side T** table and no H2D copy per call, cf. compute.h:70-72);
 //  * the output is 16-B aligned by peeling a scalar head; inputs may be
 //    mutually misaligned (partition() element offsets, reduce.h:401-415):
 //    gfx950 serves unaligned dwordx4 loads in hardware;
 //  * a batched plan kernel runs every compute of a pipeline step in ONE launch
 //    from a device descriptor table (vs one kernel + one stream + one
-//    hipStreamSynchronize per compute, compute.h:141-171).
+//    hipStreamSynchronize per compute, compute.h:87-117).
 //
 // Layout / roofline / measured numbers: DESIGN.md.
 
@@ -114,6 +114,19 @@ __device__ __forceinline__ uint16_t bf_round(float f) {
   return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 
+// Scalar head/tail accesses through the GLOBAL address space: a generic
+// pointer becomes a flat access, and a flat load pending anywhere inside the
+// plan kernel's unit loop makes the waitcnt pass treat vmcnt as out of order
+// -- every tile's adds then waited with vmcnt(0) instead of a staircase.
+template <class T>
+__device__ __forceinline__ T gld(const char *p) {
+  return *(const __attribute__((address_space(1))) T *)p;
+}
+template <class T>
+__device__ __forceinline__ void gst(char *p, T v) {
+  *(__attribute__((address_space(1))) T *)p = v;
+}
+
 // ------------------------------------------------------------ element ops --
 // Each op: elem size, packet accumulator (acc_t) with zero/add/pack, and a
 // scalar accumulator for the peeled head/tail elements.  zero() + x keeps the
@@ -128,8 +141,8 @@ struct OpF32 {
   __device__ static u32x4 pack(acc_t a) { return __builtin_bit_cast(u32x4, a); }
   typedef float sacc_t;
   __device__ static sacc_t szero() { return 0.0f; }
-  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + *(const float *)p; }
-  __device__ static void sstore(char *p, sacc_t a) { *(float *)p = a; }
+  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + gld<float>(p); }
+  __device__ static void sstore(char *p, sacc_t a) { gst<float>(p, a); }
 };
 
 struct OpF64 {
@@ -141,8 +154,8 @@ struct OpF64 {
   __device__ static u32x4 pack(acc_t a) { return __builtin_bit_cast(u32x4, a); }
   typedef double sacc_t;
   __device__ static sacc_t szero() { return 0.0; }
-  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + *(const double *)p; }
-  __device__ static void sstore(char *p, sacc_t a) { *(double *)p = a; }
+  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + gld<double>(p); }
+  __device__ static void sstore(char *p, sacc_t a) { gst<double>(p, a); }
 };
 
 struct OpU64 {
@@ -154,8 +167,8 @@ struct OpU64 {
   __device__ static u32x4 pack(acc_t a) { return __builtin_bit_cast(u32x4, a); }
   typedef uint64_t sacc_t;
   __device__ static sacc_t szero() { return 0; }
-  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + *(const uint64_t *)p; }
-  __device__ static void sstore(char *p, sacc_t a) { *(uint64_t *)p = a; }
+  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + gld<uint64_t>(p); }
+  __device__ static void sstore(char *p, sacc_t a) { gst<uint64_t>(p, a); }
 };
 
 struct OpI32 {  // two's-complement wrap-around, done in unsigned
@@ -167,8 +180,8 @@ struct OpI32 {  // two's-complement wrap-around, done in unsigned
   __device__ static u32x4 pack(acc_t a) { return a; }
   typedef uint32_t sacc_t;
   __device__ static sacc_t szero() { return 0u; }
-  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + *(const uint32_t *)p; }
-  __device__ static void sstore(char *p, sacc_t a) { *(uint32_t *)p = a; }
+  __device__ static sacc_t sadd(sacc_t a, const char *p) { return a + gld<uint32_t>(p); }
+  __device__ static void sstore(char *p, sacc_t a) { gst<uint32_t>(p, a); }
 };
 
 // bf16, reference semantics: acc is bf16, every add = f32 add then round to
@@ -201,10 +214,10 @@ struct OpBF16 {
   typedef float sacc_t;
   __device__ static sacc_t szero() { return 0.0f; }
   __device__ static sacc_t sadd(sacc_t a, const char *p) {
-    float s = a + __uint_as_float((uint32_t)(*(const uint16_t *)p) << 16);
+    float s = a + __uint_as_float((uint32_t)(gld<uint16_t>(p)) << 16);
     return __uint_as_float((uint32_t)bf_round(s) << 16);
   }
-  __device__ static void sstore(char *p, sacc_t a) { *(uint16_t *)p = bf_round(a); }
+  __device__ static void sstore(char *p, sacc_t a) { gst<uint16_t>(p, bf_round(a)); }
 };
 
 // bf16 inputs, f32 accumulator, one rounding at the end (HICCL_ACC_WIDE).
@@ -230,9 +243,9 @@ struct OpBF16Wide {
   typedef float sacc_t;
   __device__ static sacc_t szero() { return 0.0f; }
   __device__ static sacc_t sadd(sacc_t a, const char *p) {
-    return a + __uint_as_float((uint32_t)(*(const uint16_t *)p) << 16);
+    return a + __uint_as_float((uint32_t)(gld<uint16_t>(p)) << 16);
   }
-  __device__ static void sstore(char *p, sacc_t a) { *(uint16_t *)p = bf_round(a); }
+  __device__ static void sstore(char *p, sacc_t a) { gst<uint16_t>(p, bf_round(a)); }
 };
 
 // Exact byte copy (HICCL_BYTES): one input, out = in[0] bit for bit.  The
@@ -246,8 +259,8 @@ struct OpRaw {
   __device__ static u32x4 pack(acc_t a) { return a; }
   typedef uint8_t sacc_t;
   __device__ static sacc_t szero() { return 0; }
-  __device__ static sacc_t sadd(sacc_t, const char *p) { return *(const uint8_t *)p; }
-  __device__ static void sstore(char *p, sacc_t a) { *(uint8_t *)p = a; }
+  __device__ static sacc_t sadd(sacc_t, const char *p) { return gld<uint8_t>(p); }
+  __device__ static void sstore(char *p, sacc_t a) { gst<uint8_t>(p, a); }
 };
 
 // ----------------------------------------------------------- tile engine --
@@ -276,12 +289,26 @@ struct SingleArgs {
 // Descriptor of one compute in a batched plan (device memory).
 struct PlanDesc {
   char *out;
-  const char *const *in;  // device table of n input pointers
   uint64_t npkt;
-  uint64_t tile_begin;  // first global tile of this compute
+  uint64_t tile_begin;  // first global unit of this compute
   uint32_t n, head, tail, pad;
 };
-static_assert(sizeof(PlanDesc) == 48, "PlanDesc layout");
+static_assert(sizeof(PlanDesc) == 40, "PlanDesc layout");
+
+// A plan launch.  One device block holds [desc | ptrs | unit_comp]:
+//   desc[c]                  compute c
+//   ptrs[c * stride + k]     input k of compute c (stride = the plan's max n)
+//   unit_comp[t]             the compute owning global unit t (NULL: compute 0)
+// so a workgroup reaches a unit's input pointers in two dependent scalar
+// loads: unit_comp[t], then desc[c] and ptrs[c * stride ...] side by side.
+struct PlanArgs {
+  const PlanDesc *desc;
+  const char *const *ptrs;
+  const uint32_t *unit_comp;
+  uint64_t t_begin, t_end;
+  uint32_t *sched;  // dynamic unit counter, or NULL
+  uint32_t stride, grab;
+};
 
 // Input pointer source: kernarg array or device table.
 struct ArgInputs {
@@ -311,10 +338,17 @@ __device__ __forceinline__ void group_at(typename Op::acc_t (&acc)[U], Inputs in
 #pragma unroll
   for (int j = 0; j < G; j++) r[j] = make_rsrc(in(g + j) + tile_off, tile_bytes);
   u32x4 x[G][U];
+  // Every load of the group is issued before the first add, input by input
+  // (the barriers pin that order, so the adds -- input 0 first -- wait with
+  // a vmcnt staircase instead of one vmcnt(0)).  Without them the scheduler
+  // of the plan kernel (pointer table in memory) split an 8-input group into
+  // 24 + 8 (f32) or 16 + 16 (bf16) loads with an s_waitcnt vmcnt(0) in
+  // between: two memory round trips per tile.
 #pragma unroll
   for (int j = 0; j < G; j++) {
 #pragma unroll
     for (int u = 0; u < U; u++) x[j][u] = load_pkt<POL>(r[j], voff[u]);
+    __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int j = 0; j < G; j++) {
@@ -540,49 +574,38 @@ struct TableInputs {
   __device__ const char *operator()(int k) const { return ((ConstPtr *)p)[k]; }
 };
 
-// Compute owning global unit t: the c' >= c with desc[c'].tile_begin <= t <
-// desc[c'+1].tile_begin (desc[ncomp] is the sentinel).  Galloping then
-// binary search: ~2 log2(advance) dependent scalar loads (a grid-stride step
-// can skip hundreds of small computes).
-__device__ __forceinline__ uint32_t find_comp(const PlanDesc *__restrict__ desc, uint32_t c,
-                                              uint32_t ncomp, uint64_t t) {
-  if (t < desc[c + 1].tile_begin) return c;
-  uint32_t lo = c + 1, step = 1, hi;
-  while (true) {  // invariant: desc[lo].tile_begin <= t
-    const uint32_t probe = lo + step;
-    if (probe >= ncomp || t < desc[probe].tile_begin) {
-      hi = probe < ncomp ? probe : ncomp;
-      break;
-    }
-    lo = probe;
-    step <<= 1;
-  }
-  while (hi - lo > 1) {  // desc[lo].tile_begin <= t < desc[hi].tile_begin
-    const uint32_t mid = lo + (hi - lo) / 2;
-    if (desc[mid].tile_begin <= t) lo = mid; else hi = mid;
-  }
-  return lo;
+typedef const PlanDesc __attribute__((address_space(4))) ConstDesc;
+typedef const uint32_t __attribute__((address_space(4))) ConstU32;
+
+__device__ __forceinline__ PlanDesc load_desc(const PlanDesc *desc, uint32_t c) {
+  const ConstDesc *q = (const ConstDesc *)desc + c;  // scalar loads
+  PlanDesc d;
+  d.out = q->out;
+  d.npkt = q->npkt;
+  d.tile_begin = q->tile_begin;
+  d.n = q->n;
+  d.head = q->head;
+  d.tail = q->tail;
+  d.pad = 0;
+  return d;
 }
 
-// All computes of a plan in one launch.  Global tile t belongs to compute c
-// with desc[c].tile_begin <= t < desc[c+1].tile_begin (desc[ncomp] is a
-// sentinel); c only grows along a workgroup's grid-stride walk.
+// All computes of a plan in one launch.  Global unit t belongs to compute
+// unit_comp[t] (the host's table: one scalar load, instead of a search over
+// the computes' first units whose dependent probes cost several
+// microseconds in the first unit of every workgroup of a small plan).
 template <class Op, int BLOCK, int U, int POL, int ENG>
-__global__ __launch_bounds__(BLOCK) void k_reduce_plan(const PlanDesc *__restrict__ desc,
-                                                       uint32_t c_first, uint32_t ncomp,
-                                                       uint64_t t_begin, uint64_t t_end,
-                                                       uint32_t *sched, uint32_t grab) {
+__global__ __launch_bounds__(BLOCK) void k_reduce_plan(PlanArgs a) {
   const int tid = threadIdx.x;
   uint32_t voff[U];
 #pragma unroll
   for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * BLOCK + tid) * kPacket);
   constexpr uint64_t TILE = (uint64_t)BLOCK * U;
-  uint32_t c = c_first;  // units arrive in increasing order (static or dynamic)
-  for_each_unit(sched, grab, t_begin, t_end, [&](uint64_t t, auto hook) {
-    c = find_comp(desc, c, ncomp, t);
-    const PlanDesc d = desc[c];
+  for_each_unit(a.sched, a.grab, a.t_begin, a.t_end, [&](uint64_t t, auto hook) {
+    const uint32_t c = a.unit_comp ? ((ConstU32 *)a.unit_comp)[t] : 0u;
+    const PlanDesc d = load_desc(a.desc, c);
     const uint64_t lt = t - d.tile_begin;
-    TableInputs raw{d.in};
+    TableInputs raw{a.ptrs + (uint64_t)c * a.stride};
     if (lt == 0) scalar_part<Op>(d.out, raw, d.n, d.head, d.npkt, d.tail, tid);
     const uint64_t pkt0 = lt * TILE;
     if (pkt0 >= d.npkt) {  // a scalar-only compute: nothing to load or store
@@ -750,14 +773,31 @@ uint32_t default_grab(int engine, double n) {
 // the ones on slow channels straggle: 5.6-5.7 vs 6.3-6.7 TB/s on C2); never
 // during stream capture (a replayed graph could run beside other work on
 // the same stream's counter); NULL also on any allocation failure.
+// Is `s` being captured into a graph?  `if_unknown` is the answer when the
+// runtime cannot tell.
+bool capturing(hipStream_t s, bool if_unknown) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess) {
+    (void)hipGetLastError();
+    return if_unknown;
+  }
+  return cap != hipStreamCaptureStatusNone;
+}
+
+// hipStreamPerThread is one handle value for a different stream on every
+// host thread: two threads could run kernels on one counter at once (units
+// skipped, wrong sums), so it takes the static schedule.  The null stream is
+// the legacy stream here (this library is built without per-thread default
+// streams): launches on it serialise, one counter is safe.
+bool per_thread_stream(hipStream_t s) { return s == hipStreamPerThread; }
+
 uint32_t *unit_sched_for(int engine, double n, uint64_t units, uint64_t grid, int dev, hipStream_t s,
                          int schedule = HICCL_SCHED_AUTO, uint32_t grab = 0) {
   if (schedule == HICCL_SCHED_STATIC) return nullptr;
   if (schedule == HICCL_SCHED_AUTO && (engine != HICCL_ENGINE_TILE || n < kDynMinInputs)) return nullptr;
   if (!grab) grab = default_grab(engine, n);
   if ((units + grab - 1) / grab < kDynMinUnitsPerWG * grid) return nullptr;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
+  if (per_thread_stream(s) || capturing(s, true)) return nullptr;
   std::lock_guard<std::mutex> lk(g_sched_mu);
   auto it = g_sched.find(SchedKey{dev, s});
   if (it != g_sched.end()) return it->second;
@@ -1024,46 +1064,72 @@ single_fn pick_single_dtype(int dtype, const Cfg &c) {
   }
 }
 
-// ---- plan dispatch (default shapes of the two engines)
+// ---- plan dispatch
+//
+// Plan kernels (and one-shot calls with > 64 inputs, which run as a
+// one-compute plan) come in the PHASE engine's default shape and the TILE
+// engine at 256 lanes x U packets, U = 4 for every type and also 1 or 2 for
+// the headline types (f32, bf16 native).  Cache policy: nt loads and stores.
 
 constexpr int kPlanBlock = kDefBlock;
-constexpr int kPlanUnroll = kDefUnroll;
-constexpr int kPlanBpc = 1;
 
-// Packets per work unit (tile or chunk) of a plan launched with `engine`.
-uint64_t unit_pkts(int engine, int dtype, int acc) {
+// Packets per work unit (tile or chunk) of a plan kernel.
+uint64_t unit_pkts(int engine, int dtype, int acc, int unroll) {
   return engine == HICCL_ENGINE_PHASE ? (uint64_t)kPhBlock * phase_p_dtype(dtype, acc)
-                                      : (uint64_t)kPlanBlock * kPlanUnroll;
+                                      : (uint64_t)kPlanBlock * (unroll ? unroll : kDefUnroll);
 }
 
-typedef void (*plan_fn)(const PlanDesc *, uint32_t, uint32_t, uint64_t, uint64_t, uint32_t *, uint32_t,
-                        dim3, hipStream_t);
+typedef void (*plan_fn)(const PlanArgs &, dim3, hipStream_t);
 
-template <class Op, int ENG>
-void launch_plan_t(const PlanDesc *d, uint32_t c0, uint32_t ncomp, uint64_t t0, uint64_t t1,
-                   uint32_t *sched, uint32_t grab, dim3 grid, hipStream_t s) {
+template <class Op, int ENG, int U>
+void launch_plan_t(const PlanArgs &a, dim3 grid, hipStream_t s) {
   constexpr int B = ENG == kPhase ? kPhBlock : kPlanBlock;
-  constexpr int U = ENG == kPhase ? phase_p<Op>() : kPlanUnroll;
-  hipLaunchKernelGGL((k_reduce_plan<Op, B, U, kDefPol, ENG>), grid, dim3(B), 0, s, d, c0, ncomp, t0, t1,
-                     sched, grab);
+  hipLaunchKernelGGL((k_reduce_plan<Op, B, U, kDefPol, ENG>), grid, dim3(B), 0, s, a);
 }
 
-template <class Op>
-plan_fn pick_plan_eng(int engine) {
-  return engine == HICCL_ENGINE_PHASE ? launch_plan_t<Op, kPhase> : launch_plan_t<Op, kTile>;
+template <class Op, bool TUNED>
+plan_fn pick_plan_eng(int engine, int unroll) {
+  if (engine == HICCL_ENGINE_PHASE) return launch_plan_t<Op, kPhase, phase_p<Op>()>;
+  switch (unroll) {
+    case 0:
+    case 4: return launch_plan_t<Op, kTile, 4>;
+    case 2: if constexpr (TUNED) return launch_plan_t<Op, kTile, 2>; break;
+    case 1: if constexpr (TUNED) return launch_plan_t<Op, kTile, 1>; break;
+    default: break;
+  }
+  return nullptr;
 }
 
-plan_fn pick_plan(int dtype, int acc, int engine) {
+plan_fn pick_plan(int dtype, int acc, int engine, int unroll) {
   switch (dtype) {
-    case HICCL_FLOAT32: return pick_plan_eng<OpF32>(engine);
+    case HICCL_FLOAT32: return pick_plan_eng<OpF32, true>(engine, unroll);
     case HICCL_BFLOAT16:
-      return acc == HICCL_ACC_WIDE ? pick_plan_eng<OpBF16Wide>(engine) : pick_plan_eng<OpBF16>(engine);
-    case HICCL_FLOAT64: return pick_plan_eng<OpF64>(engine);
-    case HICCL_UINT64: return pick_plan_eng<OpU64>(engine);
-    case HICCL_INT32: return pick_plan_eng<OpI32>(engine);
-    case HICCL_BYTES: return pick_plan_eng<OpRaw>(engine);
+      return acc == HICCL_ACC_WIDE ? pick_plan_eng<OpBF16Wide, false>(engine, unroll)
+                                   : pick_plan_eng<OpBF16, true>(engine, unroll);
+    case HICCL_FLOAT64: return pick_plan_eng<OpF64, false>(engine, unroll);
+    case HICCL_UINT64: return pick_plan_eng<OpU64, false>(engine, unroll);
+    case HICCL_INT32: return pick_plan_eng<OpI32, false>(engine, unroll);
+    case HICCL_BYTES: return pick_plan_eng<OpRaw, false>(engine, unroll);
     default: return nullptr;
   }
+}
+
+// Is `c` (engine resolved, shape filled in by finish_cfg) a shape the plan
+// kernels have?  Empty string if so, else why not.
+std::string plan_shape_error(const Cfg &c, int dtype) {
+  if (c.nt != kDefPol % 10 || c.store != kDefPol / 10)
+    return "plan kernels use nt loads and nt stores only (nontemporal 2, store_policy 2)";
+  if (c.drain) return "plan kernels do not support drain";
+  if (c.engine == HICCL_ENGINE_PHASE) {
+    if (c.block != kPhBlock || c.unroll != phase_p_dtype(dtype, c.acc))
+      return "plan kernels run the PHASE engine in its default shape only (block 512, unroll " +
+             std::to_string(phase_p_dtype(dtype, c.acc)) + ")";
+    return "";
+  }
+  if (c.block != kPlanBlock) return "plan kernels run the TILE engine at block 256 only";
+  if (!pick_plan(dtype, c.acc, HICCL_ENGINE_TILE, c.unroll))
+    return "plan kernels run the TILE engine at unroll 4 (f32 / bf16: 1, 2 or 4) only";
+  return "";
 }
 
 uint64_t tiles_for(uint64_t npkt, uint64_t tile) {
@@ -1073,8 +1139,9 @@ uint64_t tiles_for(uint64_t npkt, uint64_t tile) {
 
 // Large-n one-shot path: stage the pointer table in stream-ordered device
 // memory and run it as a one-compute plan.
-int reduce_via_table(int dtype, int acc, int engine, void *out, const void *const *in, int n,
-                     size_t count, hipStream_t s);
+int reduce_via_table(int dtype, const Cfg &c, void *out, const void *const *in, int n, size_t count,
+                     hipStream_t s);
+
 
 }  // namespace
 
@@ -1109,7 +1176,18 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
   const int dev = current_device();
   Split sp = split_on(out, count, esz);
   finish_cfg(c, sp.npkt, n, dtype, dev);
-  if (n > kMaxArgInputs) return reduce_via_table(dtype, c.acc, c.engine, out, in, n, count, s);
+  if (c.bpc < 1 || c.bpc > 64) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: blocks_per_cu");
+  if (c.grid < 0) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: grid < 0");
+  if (n > kMaxArgInputs) {
+    const std::string why = plan_shape_error(c, dtype);
+    if (!why.empty()) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: n > 64 inputs run on the plan kernel: " + why);
+    // the > 64-input pointer table is uploaded from host memory per call: a
+    // captured graph would replay a copy from a freed host buffer
+    if (capturing(s, false))
+      return fail(hipErrorStreamCaptureUnsupported,
+                  "hiccl_reduce: n > 64 inputs cannot be captured into a graph (use a plan)");
+    return reduce_via_table(dtype, c, out, in, n, count, s);
+  }
 
   single_fn fn = pick_single_dtype(dtype, c);
   if (!fn)
@@ -1119,8 +1197,6 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
                                           std::to_string(c.nt) + ", store " +
                                           std::to_string(c.store) + ", engine " +
                                           std::to_string(c.engine) + ") for this dtype");
-  if (c.bpc < 1 || c.bpc > 64) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: blocks_per_cu");
-  if (c.grid < 0) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: grid < 0");
 
   SingleArgs a;
   memset(&a, 0, sizeof(a));
@@ -1162,11 +1238,11 @@ int hiccl_reduce_bf16(uint16_t *out, const uint16_t *const *in, int n, size_t co
 struct hiccl_reduce_plan {
   int dtype = 0;
   int device = 0;
-  int acc = HICCL_ACC_NATIVE;
-  int engine_req = HICCL_ENGINE_AUTO;  // hiccl_reduce_plan_set_engine
-  int engine = HICCL_ENGINE_TILE;      // resolved at upload
-  double mean_n = 0;                   // packet-weighted inputs per compute
-  int bpc = 1;                         // workgroups per CU, resolved at upload
+  hiccl_reduce_config_t req;      // hiccl_reduce_plan_set_config / _set_engine / _set_acc (0 = default)
+  int engine = HICCL_ENGINE_TILE;  // resolved at upload
+  int unroll = kDefUnroll;         // TILE packets per lane, resolved at upload
+  double mean_n = 0;               // packet-weighted inputs per compute
+  int bpc = 1;                     // workgroups per CU, resolved at upload
   size_t esz = 0;
   struct Comp {
     void *out;
@@ -1174,11 +1250,10 @@ struct hiccl_reduce_plan {
     size_t count;
   };
   std::vector<Comp> comps;
-  std::vector<PlanDesc> host_desc;  // numcomp + 1 (sentinel)
   int maxn = 0;
   bool dirty = true;
-  PlanDesc *d_desc = nullptr;
-  const void **d_ptrs = nullptr;
+  char *d_block = nullptr;  // [desc | ptrs | unit_comp] (PlanArgs)
+  PlanArgs args;            // pointers into d_block
   uint64_t total_tiles = 0;
   hipStream_t own = nullptr;
   hipEvent_t done = nullptr;
@@ -1187,108 +1262,159 @@ struct hiccl_reduce_plan {
 
 namespace {
 
-int plan_upload(hiccl_reduce_plan *p) {
+// The plan's configuration with its engine and shape resolved for `npkt`
+// packets of packet-weighted mean `mean_n` inputs.
+Cfg plan_cfg(const hiccl_reduce_plan *p, uint64_t npkt, double mean_n) {
+  Cfg c = resolve(&p->req);
+  if (c.engine == HICCL_ENGINE_AUTO)
+    c.engine = (c.block || c.unroll) ? HICCL_ENGINE_TILE : auto_engine(npkt, mean_n, p->dtype, c.acc, p->device);
+  if (c.engine == HICCL_ENGINE_PHASE) {
+    if (!c.block) c.block = kPhBlock;
+    if (!c.unroll) c.unroll = phase_p_dtype(p->dtype, c.acc);
+  } else {
+    if (!c.block) c.block = kPlanBlock;
+    if (!c.unroll) c.unroll = kDefUnroll;
+  }
+  if (!c.bpc) c.bpc = auto_bpc(c.engine, npkt, p->dtype, c.acc, p->device);
+  return c;
+}
+
+// Lay out [desc (ncomp) | ptrs (ncomp x stride) | unit_comp (units)] on the
+// host, 8-B aligned pieces; returns the byte size, fills the offsets.
+struct BlockLayout {
+  size_t desc, ptrs, unit_comp, bytes;
+};
+BlockLayout block_layout(size_t ncomp, size_t stride, size_t units) {
+  BlockLayout L;
+  L.desc = 0;
+  L.ptrs = ncomp * sizeof(PlanDesc);
+  L.unit_comp = L.ptrs + ncomp * stride * sizeof(void *);
+  L.bytes = L.unit_comp + ((units * sizeof(uint32_t) + 7) & ~(size_t)7);
+  return L;
+}
+
+int plan_upload(hiccl_reduce_plan *p, hipStream_t s) {
   if (!p->dirty) return 0;
-  if (p->d_desc) { (void)hipFree(p->d_desc); p->d_desc = nullptr; }
-  if (p->d_ptrs) { (void)hipFree(p->d_ptrs); p->d_ptrs = nullptr; }
+  // synchronous allocation + copy: not allowed inside a stream capture
+  // (capture a plan only after a launch outside the capture uploaded it)
+  if (capturing(s, false))
+    return fail(hipErrorStreamCaptureUnsupported,
+                "plan: the first launch after an add or a config change uploads the plan and cannot be captured");
+  if (p->d_block) {
+    if (p->launched) (void)hipEventSynchronize(p->done);  // a running launch still reads it
+    (void)hipFree(p->d_block);
+    p->d_block = nullptr;
+  }
   const size_t nc = p->comps.size();
-  size_t nptr = 0;
-  for (auto &c : p->comps) nptr += c.in.size();
-  std::vector<const void *> ptrs;
-  ptrs.reserve(nptr ? nptr : 1);
-  for (auto &c : p->comps) ptrs.insert(ptrs.end(), c.in.begin(), c.in.end());
-  if (ptrs.empty()) ptrs.push_back(nullptr);
-  if (int e = check_hip(hipMalloc((void **)&p->d_ptrs, ptrs.size() * sizeof(void *)), "plan: hipMalloc ptrs"))
-    return e;
-  if (int e = check_hip(hipMemcpy(p->d_ptrs, ptrs.data(), ptrs.size() * sizeof(void *),
-                                  hipMemcpyHostToDevice), "plan: upload ptrs"))
-    return e;
-  p->host_desc.assign(nc + 1, PlanDesc{});
   uint64_t total_pkt = 0;
   double weighted_n = 0;
+  p->maxn = 0;
   for (auto &c : p->comps) {
     const uint64_t k = split_on(c.out, c.count, p->esz).npkt;
     total_pkt += k;
     weighted_n += (double)k * c.in.size();
+    if ((int)c.in.size() > p->maxn) p->maxn = (int)c.in.size();
   }
   const double mean_n = total_pkt ? weighted_n / total_pkt : 0;
   p->mean_n = mean_n;
-  p->engine = p->engine_req != HICCL_ENGINE_AUTO
-                  ? p->engine_req
-                  : auto_engine(total_pkt, mean_n, p->dtype, p->acc, p->device);
-  p->bpc = auto_bpc(p->engine, total_pkt, p->dtype, p->acc, p->device);
-  const uint64_t unit = unit_pkts(p->engine, p->dtype, p->acc);
+  const Cfg c = plan_cfg(p, total_pkt, mean_n);
+  p->engine = c.engine;
+  p->unroll = c.unroll;
+  p->bpc = c.bpc;
+  const uint64_t unit = unit_pkts(p->engine, p->dtype, c.acc, p->unroll);
+  uint64_t units = 0;
+  for (auto &cp : p->comps) units += tiles_for(split_on(cp.out, cp.count, p->esz).npkt, unit);
+  const size_t stride = p->maxn > 0 ? (size_t)p->maxn : 1;
+  const BlockLayout L = block_layout(nc, stride, units);
+  std::vector<char> host(L.bytes, 0);
+  PlanDesc *hd = (PlanDesc *)(host.data() + L.desc);
+  const void **hp = (const void **)(host.data() + L.ptrs);
+  uint32_t *hu = (uint32_t *)(host.data() + L.unit_comp);
   uint64_t tile = 0;
-  size_t off = 0;
-  p->maxn = 0;
   for (size_t i = 0; i < nc; i++) {
-    auto &c = p->comps[i];
-    Split sp = split_on(c.out, c.count, p->esz);
-    PlanDesc &d = p->host_desc[i];
-    d.out = (char *)c.out;
-    d.in = (const char *const *)(p->d_ptrs + off);
+    auto &cp = p->comps[i];
+    Split sp = split_on(cp.out, cp.count, p->esz);
+    PlanDesc &d = hd[i];
+    d.out = (char *)cp.out;
     d.npkt = sp.npkt;
     d.head = sp.head;
     d.tail = sp.tail;
-    d.n = (uint32_t)c.in.size();
+    d.n = (uint32_t)cp.in.size();
     d.tile_begin = tile;
-    tile += tiles_for(sp.npkt, unit);
-    off += c.in.size();
-    if ((int)c.in.size() > p->maxn) p->maxn = (int)c.in.size();
+    for (size_t k = 0; k < cp.in.size(); k++) hp[i * stride + k] = cp.in[k];
+    const uint64_t nt = tiles_for(sp.npkt, unit);
+    for (uint64_t t = 0; t < nt; t++) hu[tile + t] = (uint32_t)i;
+    tile += nt;
   }
-  p->host_desc[nc].tile_begin = UINT64_MAX;  // sentinel
   p->total_tiles = tile;
-  if (int e = check_hip(hipMalloc((void **)&p->d_desc, (nc + 1) * sizeof(PlanDesc)), "plan: hipMalloc desc"))
+  if (int e = check_hip(hipMalloc((void **)&p->d_block, L.bytes), "plan: hipMalloc")) return e;
+  if (int e = check_hip(hipMemcpy(p->d_block, host.data(), L.bytes, hipMemcpyHostToDevice), "plan: upload"))
     return e;
-  if (int e = check_hip(hipMemcpy(p->d_desc, p->host_desc.data(), (nc + 1) * sizeof(PlanDesc),
-                                  hipMemcpyHostToDevice), "plan: upload desc"))
-    return e;
+  memset(&p->args, 0, sizeof(p->args));
+  p->args.desc = (const PlanDesc *)(p->d_block + L.desc);
+  p->args.ptrs = (const char *const *)(p->d_block + L.ptrs);
+  p->args.unit_comp = nc > 1 ? (const uint32_t *)(p->d_block + L.unit_comp) : nullptr;
+  p->args.stride = (uint32_t)stride;
+  p->args.t_begin = 0;
+  p->args.t_end = tile;
   p->dirty = false;
   return 0;
 }
 
-int plan_kernel(hiccl_reduce_plan *p, uint32_t c0, uint64_t t0, uint64_t t1, int maxn,
-                hipStream_t s) {
-  plan_fn fn = pick_plan(p->dtype, p->acc, p->engine);
-  if (!fn) return fail(hipErrorInvalidValue, "plan: unsupported dtype");
-  uint64_t grid = (uint64_t)device_cus(p->device) * p->bpc;
-  if (grid > t1 - t0) grid = t1 - t0;
-  fn(p->d_desc, c0, (uint32_t)p->comps.size(), t0, t1,
-     unit_sched_for(p->engine, p->mean_n, t1 - t0, grid, p->device, s), default_grab(p->engine, p->mean_n),
-     dim3((unsigned)grid), s);
+// One plan-kernel launch of `a` (desc, ptrs, unit_comp, units, stride set),
+// shaped by `c` (engine and shape resolved).
+int launch_plan(PlanArgs a, int dtype, const Cfg &c, double mean_n, int dev, hipStream_t s) {
+  plan_fn fn = pick_plan(dtype, c.acc, c.engine, c.unroll);
+  if (!fn) return fail(hipErrorInvalidValue, "plan: unsupported dtype / shape");
+  const uint64_t units = a.t_end - a.t_begin;
+  uint64_t grid = c.grid > 0 ? (uint64_t)c.grid : (uint64_t)device_cus(dev) * c.bpc;
+  if (grid > units) grid = units;
+  a.grab = c.grab > 0 ? (uint32_t)c.grab : default_grab(c.engine, mean_n);
+  a.sched = unit_sched_for(c.engine, mean_n, units, grid, dev, s, c.schedule, a.grab);
+  fn(a, dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "plan: launch");
 }
 
-int reduce_via_table(int dtype, int acc, int engine, void *out, const void *const *in, int n,
-                     size_t count, hipStream_t s) {
+int plan_kernel(hiccl_reduce_plan *p, hipStream_t s) {
+  Cfg c = resolve(&p->req);
+  c.engine = p->engine;
+  c.unroll = p->unroll;
+  c.block = p->engine == HICCL_ENGINE_PHASE ? kPhBlock : kPlanBlock;
+  c.bpc = p->bpc;
+  return launch_plan(p->args, p->dtype, c, p->mean_n, p->device, s);
+}
+
+int reduce_via_table(int dtype, const Cfg &c, void *out, const void *const *in, int n, size_t count,
+                     hipStream_t s) {
   const size_t esz = esize(dtype);
   Split sp = split_on(out, count, esz);
-  const size_t bytes = 2 * sizeof(PlanDesc) + (size_t)n * sizeof(void *);
-  std::vector<char> host(bytes, 0);
-  PlanDesc *hd = (PlanDesc *)host.data();
-  const void **hp = (const void **)(host.data() + 2 * sizeof(PlanDesc));
+  const BlockLayout L = block_layout(1, (size_t)n, 0);
+  std::vector<char> host(L.bytes, 0);
+  PlanDesc *hd = (PlanDesc *)(host.data() + L.desc);
+  const void **hp = (const void **)(host.data() + L.ptrs);
   for (int k = 0; k < n; k++) hp[k] = in[k];
+  hd->out = (char *)out;
+  hd->npkt = sp.npkt;
+  hd->head = sp.head;
+  hd->tail = sp.tail;
+  hd->n = (uint32_t)n;
+  hd->tile_begin = 0;
   char *dmem = nullptr;
-  if (int e = check_hip(hipMallocAsync((void **)&dmem, bytes, s), "hiccl_reduce: hipMallocAsync"))
-    return e;
-  hd[0].out = (char *)out;
-  hd[0].in = (const char *const *)(dmem + 2 * sizeof(PlanDesc));
-  hd[0].npkt = sp.npkt;
-  hd[0].head = sp.head;
-  hd[0].tail = sp.tail;
-  hd[0].n = (uint32_t)n;
-  hd[0].tile_begin = 0;
-  const uint64_t tiles = tiles_for(sp.npkt, unit_pkts(engine, dtype, acc));
-  hd[1].tile_begin = UINT64_MAX;
-  if (int e = check_hip(hipMemcpyAsync(dmem, host.data(), bytes, hipMemcpyHostToDevice, s),
+  if (int e = check_hip(hipMallocAsync((void **)&dmem, L.bytes, s), "hiccl_reduce: hipMallocAsync")) return e;
+  // hipMemcpyAsync from pageable memory returns once the source is consumed,
+  // so `host` may go out of scope (never under capture: refused by the caller)
+  if (int e = check_hip(hipMemcpyAsync(dmem, host.data(), L.bytes, hipMemcpyHostToDevice, s),
                         "hiccl_reduce: table upload"))
     return e;
-  plan_fn fn = pick_plan(dtype, acc, engine);
-  uint64_t grid = (uint64_t)device_cus(current_device()) * kPlanBpc;
-  if (grid > tiles) grid = tiles;
-  fn((const PlanDesc *)dmem, 0, 1, 0, tiles, unit_sched_for(engine, n, tiles, grid, current_device(), s),
-     default_grab(engine, n), dim3((unsigned)grid), s);
-  if (int e = check_hip(hipGetLastError(), "hiccl_reduce: launch")) return e;
+  PlanArgs a;
+  memset(&a, 0, sizeof(a));
+  a.desc = (const PlanDesc *)(dmem + L.desc);
+  a.ptrs = (const char *const *)(dmem + L.ptrs);
+  a.unit_comp = nullptr;
+  a.stride = (uint32_t)n;
+  a.t_begin = 0;
+  a.t_end = tiles_for(sp.npkt, unit_pkts(c.engine, dtype, c.acc, c.unroll));
+  if (int e = launch_plan(a, dtype, c, n, current_device(), s)) return e;
   return check_hip(hipFreeAsync(dmem, s), "hiccl_reduce: hipFreeAsync");
 }
 
@@ -1305,6 +1431,7 @@ int hiccl_reduce_plan_create(hiccl_reduce_plan_t **plan, int dtype, int device) 
   if (device < 0 || device >= ndev) return fail(hipErrorInvalidDevice, "plan_create: bad device");
   if (int e = check_hip(hipSetDevice(device), "plan_create: hipSetDevice")) return e;
   auto *p = new hiccl_reduce_plan;
+  memset(&p->req, 0, sizeof(p->req));
   p->dtype = dtype;
   p->device = device;
   p->esz = esize(dtype);
@@ -1322,7 +1449,7 @@ int hiccl_reduce_plan_set_acc(hiccl_reduce_plan_t *p, int acc) {
   if (!p) return fail(hipErrorInvalidValue, "plan_set_acc: plan is NULL");
   if (acc != HICCL_ACC_NATIVE && acc != HICCL_ACC_WIDE)
     return fail(hipErrorInvalidValue, "plan_set_acc: bad mode");
-  p->acc = acc;
+  p->req.acc = acc;
   p->dirty = true;  // the auto engine's chunk size depends on the accumulator
   return 0;
 }
@@ -1331,7 +1458,39 @@ int hiccl_reduce_plan_set_engine(hiccl_reduce_plan_t *p, int engine) {
   if (!p) return fail(hipErrorInvalidValue, "plan_set_engine: plan is NULL");
   if (engine < HICCL_ENGINE_AUTO || engine > HICCL_ENGINE_PHASE)
     return fail(hipErrorInvalidValue, "plan_set_engine: bad engine");
-  p->engine_req = engine;
+  p->req.engine = engine;
+  p->dirty = true;
+  return 0;
+}
+
+int hiccl_reduce_plan_set_config(hiccl_reduce_plan_t *p, const hiccl_reduce_config_t *cfg) {
+  if (!p) return fail(hipErrorInvalidValue, "plan_set_config: plan is NULL");
+  hiccl_reduce_config_t z;
+  memset(&z, 0, sizeof(z));
+  const hiccl_reduce_config_t &c = cfg ? *cfg : z;
+  if (c.acc != HICCL_ACC_NATIVE && c.acc != HICCL_ACC_WIDE) return fail(hipErrorInvalidValue, "plan_set_config: bad acc");
+  if (c.engine < HICCL_ENGINE_AUTO || c.engine > HICCL_ENGINE_PHASE)
+    return fail(hipErrorInvalidValue, "plan_set_config: bad engine");
+  if (c.schedule < HICCL_SCHED_AUTO || c.schedule > HICCL_SCHED_DYNAMIC)
+    return fail(hipErrorInvalidValue, "plan_set_config: bad schedule");
+  if (c.grab < 0 || c.grab > 4096) return fail(hipErrorInvalidValue, "plan_set_config: bad grab");
+  if (c.blocks_per_cu < 0 || c.blocks_per_cu > 64) return fail(hipErrorInvalidValue, "plan_set_config: blocks_per_cu");
+  if (c.grid < 0) return fail(hipErrorInvalidValue, "plan_set_config: grid < 0");
+  // the shape must be one the plan kernels have, whatever engine AUTO picks
+  Cfg r = resolve(&c);
+  const bool shape = c.block || c.unroll;
+  if (shape && r.engine == HICCL_ENGINE_AUTO) r.engine = HICCL_ENGINE_TILE;
+  const int engines[2] = {HICCL_ENGINE_TILE, HICCL_ENGINE_PHASE};
+  for (int eng : engines) {
+    if (r.engine != HICCL_ENGINE_AUTO && r.engine != eng) continue;
+    Cfg t = r;
+    t.engine = eng;
+    if (!t.block) t.block = eng == HICCL_ENGINE_PHASE ? kPhBlock : kPlanBlock;
+    if (!t.unroll) t.unroll = eng == HICCL_ENGINE_PHASE ? phase_p_dtype(p->dtype, t.acc) : kDefUnroll;
+    const std::string why = plan_shape_error(t, p->dtype);
+    if (!why.empty()) return fail(hipErrorInvalidValue, "plan_set_config: " + why);
+  }
+  p->req = c;
   p->dirty = true;
   return 0;
 }
@@ -1357,13 +1516,12 @@ int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *p, void *stream) {
   if (!p) return fail(hipErrorInvalidValue, "plan_launch: plan is NULL");
   if (int e = check_hip(hipSetDevice(p->device), "plan_launch: hipSetDevice")) return e;
   if (p->comps.empty()) return 0;
-  if (int e = plan_upload(p)) return e;
   hipStream_t s = (hipStream_t)stream;
-  if (int e = plan_kernel(p, 0, 0, p->total_tiles, p->maxn, s)) return e;
+  if (int e = plan_upload(p, s)) return e;
+  if (int e = plan_kernel(p, s)) return e;
   // a capturing stream gets no completion event (plan_sync does not apply
   // to graph replays: synchronise the stream the graph runs on)
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) return 0;
+  if (capturing(s, false)) return 0;
   p->launched = true;
   return check_hip(hipEventRecord(p->done, s), "plan_launch: event");
 }
@@ -1373,13 +1531,9 @@ int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *p, void *stream) {
   if (int e = check_hip(hipSetDevice(p->device), "plan_launch_each: hipSetDevice")) return e;
   if (p->comps.empty()) return 0;
   // One one-shot launch per compute, each with the engine AUTO picks for that
-  // compute alone (the reference's structure, compute.h:141-145).
-  hiccl_reduce_config_t cfg;
-  memset(&cfg, 0, sizeof(cfg));
-  cfg.acc = p->acc;
-  cfg.engine = p->engine_req;
+  // compute alone (the reference's structure, compute.h:88-91).
   for (auto &c : p->comps)
-    if (int e = hiccl_reduce_ex(p->dtype, c.out, c.in.data(), (int)c.in.size(), c.count, stream, &cfg))
+    if (int e = hiccl_reduce_ex(p->dtype, c.out, c.in.data(), (int)c.in.size(), c.count, stream, &p->req))
       return e;
   p->launched = true;
   return check_hip(hipEventRecord(p->done, (hipStream_t)stream), "plan_launch_each: event");
@@ -1414,8 +1568,7 @@ void hiccl_reduce_plan_destroy(hiccl_reduce_plan_t *p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
   if (p->launched) (void)hipEventSynchronize(p->done);
-  if (p->d_desc) (void)hipFree(p->d_desc);
-  if (p->d_ptrs) (void)hipFree(p->d_ptrs);
+  if (p->d_block) (void)hipFree(p->d_block);
   if (p->done) (void)hipEventDestroy(p->done);
   if (p->own) (void)hipStreamDestroy(p->own);
   delete p;

@@ -13,10 +13,19 @@ namespace HiCCL {
 
 enum collective { dummy, gather, scatter, broadcast, reduce, alltoall, allgather, reducescatter, allreduce };
 
+// Sorted per-iteration times (seconds, MAX over ranks) of measure().
+struct Times {
+  std::vector<double> t;
+  double min() const { return t.empty() ? 0 : t.front(); }
+  double median() const { return t.empty() ? 0 : t[t.size() / 2]; }
+  double max() const { return t.empty() ? 0 : t.back(); }
+};
+
 // bench.h:1-60: whole-collective time per iteration (barrier, run, MAX over
-// ranks); GB/s priced on count * sizeof(T) (the user buffer).
+// ranks); GB/s priced on count * sizeof(T) (the user buffer).  Also returns
+// the sorted times (the reference returns nothing).
 template <typename T>
-void measure(int warmup, int numiter, size_t count, Comm<T> &comm) {
+Times measure(int warmup, int numiter, size_t count, Comm<T> &comm) {
   std::vector<double> times;
   if (CommBench::myid == CommBench::printid) std::printf("%d warmup iterations (in order):\n", warmup);
   for (int it = -warmup; it < numiter; it++) {
@@ -36,6 +45,8 @@ void measure(int warmup, int numiter, size_t count, Comm<T> &comm) {
   }
   if (CommBench::myid == CommBench::printid) std::printf("Total ");
   Compute<T>::print_times(times, (double)count * sizeof(T));
+  std::sort(times.begin(), times.end());
+  return Times{times};
 }
 
 // bench.h:62-227: known-answer test.  sendbuf[i] = i on every rank, recv

@@ -15,6 +15,8 @@
 
 #include <pthread.h>
 
+#include <algorithm>
+
 #include <cstdio>
 #include <cstdlib>
 #include <list>
@@ -119,14 +121,17 @@ class Comm {
   void set_pipedepth(int d) { sch.pipedepth = d < 1 ? 1 : d; }
   void set_numstripe(int s) { sch.numstripe = s < 1 ? 1 : s; }
   void set_ringnodes(int r) { sch.ringnodes = r < 1 ? 1 : r; }
-  // Stream-ordered execution (HIP port, all ranks on one node): every step's
-  // transfers, their ready/done signalling and its compute are enqueued on
-  // the rank's stream and run() synchronises once at the end.  Opt-in
-  // (HICCL_STREAM_ORDERED=1 or this setter): on the single-GPU rehearsals we
-  // can run, ranks sharing one device serialise and the host-driven mode is
-  // faster; with one process per GPU this mode removes
-  // every host round trip per step.
-  void set_stream_ordered(bool on) { stream_req = on ? 1 : 0; }
+  // Stream-ordered execution (HIP port, all ranks on one node, one GPU per
+  // rank): every step's transfers, their ready/done signalling and its
+  // compute are enqueued on the rank's stream and run() synchronises once at
+  // the end.  Opt-in (HICCL_STREAM_ORDERED=1 or this setter).  When ranks
+  // share a device, init() falls back to host-driven mode and says so: the
+  // spinning waits of co-resident ranks can hold the device's hardware
+  // queues while a peer's queue is not mapped.
+  // `force` (HICCL_STREAM_ORDERED=force) keeps the mode anyway -- for
+  // single-GPU rehearsals with few hardware queues per process
+  // (GPU_MAX_HW_QUEUES), not for production.
+  void set_stream_ordered(bool on, bool force = false) { stream_req = on ? (force ? 2 : 1) : 0; }
   // Fused gather + reduce (HIP port, IPC / IPC_get levels): a transfer whose
   // receive buffer only feeds a reduction of the same step is not copied;
   // the reduction kernel reads the sender's buffer over xGMI in place.
@@ -221,9 +226,27 @@ class Comm {
     coll_batch = sch.factorize(P);
     libs = libraries_used(coll_batch);
     steps = merge_steps(coll_batch, libs, 1);
+#ifndef HICCL_PORT_HOST
+    shared_device = CommBench::ranks_share_device();
+    if (std::find(libs.begin(), libs.end(), CommBench::XCCL) != libs.end()) {
+      xccl = CommBench::xccl_setup(shared_device);
+      if (!xccl && CommBench::myid == CommBench::printid)
+        std::printf("HiCCL: XCCL levels run on the IPC path (%s)\n",
+#ifdef HICCL_WITH_RCCL
+                    "ranks share a GPU: RCCL needs one GPU per rank"
+#else
+                    "built without HICCL_WITH_RCCL"
+#endif
+        );
+    }
+#endif
     streamed = want_stream_mode();
     fused = want_fused();
     graphed = streamed && want_graph();
+    if (graphed && xccl) {  // RCCL groups are not recorded into the replay graph
+      graphed = false;
+      if (CommBench::myid == CommBench::printid) std::printf("HiCCL: graph replay off (XCCL level on RCCL)\n");
+    }
     CommBench::stream_ordered = streamed;
     command_batch = instantiate(steps, libs, fused);
     CommBench::stream_ordered = false;
@@ -247,10 +270,12 @@ class Comm {
     MPI_Barrier(CommBench::comm_mpi);  // nobody runs before every rank's handles are exchanged
     report_memory();
     if (CommBench::myid == CommBench::printid)
-      std::printf("initialization time: %e seconds (%zu steps, %zu libraries, %s%s%s)\n", MPI_Wtime() - t0,
+      std::printf("initialization time: %e seconds (%zu steps, %zu libraries, %s%s%s%s)\n", MPI_Wtime() - t0,
                   steps.size(), libs.size(), streamed ? "stream-ordered" : "host-driven", graphed ? ", graph replay" : "",
-                  fused ? ", fused gather" : "");
+                  fused ? ", fused gather" : "", xccl ? ", XCCL on RCCL" : "");
   }
+
+  bool xccl_on_rccl() const { return xccl; }
 
   bool stream_ordered() const { return streamed; }
   bool fused_gather() const { return fused; }
@@ -330,6 +355,43 @@ class Comm {
     }
   }
 
+#ifndef HICCL_PORT_HOST
+  // Kernel time of this rank's batched compute per step: HIP events around
+  // the step's plan launch alone on the compute stream, median of `reps`
+  // (after one warm launch), for every step in which this rank computes.
+  // Measurement only -- it overwrites the steps' outputs, so run it before
+  // (not between) the runs whose results are checked.  Returns
+  // {milliseconds, algorithmic bytes} per step.
+  std::vector<std::pair<double, size_t>> compute_kernel_times(int reps) {
+    std::vector<std::pair<double, size_t>> out;
+    CommBench::setup_gpu();
+    hipStream_t s = compute_stream();
+    hipEvent_t a, b;
+    CommBench::hip_check(hipEventCreate(&a), "hipEventCreate");
+    CommBench::hip_check(hipEventCreate(&b), "hipEventCreate");
+    for (auto &lst : command_batch)
+      for (auto &c : lst) {
+        if (!c.compute->numcomp) continue;
+        c.compute->launch(s);  // warm (and the plan's one-time upload)
+        std::vector<float> t;
+        for (int r = 0; r < std::max(reps, 1); r++) {
+          CommBench::hip_check(hipEventRecord(a, s), "hipEventRecord");
+          c.compute->launch(s);
+          CommBench::hip_check(hipEventRecord(b, s), "hipEventRecord");
+          CommBench::hip_check(hipEventSynchronize(b), "hipEventSynchronize");
+          float ms = 0;
+          CommBench::hip_check(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
+          t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        out.emplace_back((double)t[t.size() / 2], c.compute->bytes());
+      }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return out;
+  }
+#endif
+
   size_t numsteps() const { return steps.size(); }
   const std::vector<std::vector<Coll<T>>> &plan() const { return steps; }
   const Schedule<T> &schedule() const { return sch; }
@@ -345,8 +407,10 @@ class Comm {
   pthread_t thread{};
   bool running = false;
 
-  int stream_req = -1;  // -1: decide from the environment and the node layout
+  int stream_req = -1;  // -1: decide from the environment and the node layout; 2: forced
   bool streamed = false;
+  bool shared_device = false;  // two or more ranks drive one GPU
+  bool xccl = false;           // XCCL levels run on RCCL
   int fuse_req = -1;  // -1: HICCL_FUSED_GATHER
   bool fused = false;
   int graph_req = -1;  // -1: HICCL_GRAPH
@@ -469,15 +533,19 @@ class Comm {
     int on = stream_req;
     if (on < 0) {
       const char *env = std::getenv("HICCL_STREAM_ORDERED");
-      on = (env && std::string(env) == "1") ? 1 : 0;
+      const std::string v = env ? env : "";
+      on = v == "force" ? 2 : v == "1" ? 1 : 0;
     }
     MPI_Comm local;
     MPI_Comm_split_type(CommBench::comm_mpi, MPI_COMM_TYPE_SHARED, CommBench::myid, MPI_INFO_NULL, &local);
     int lsize = 0;
     MPI_Comm_size(local, &lsize);
     MPI_Comm_free(&local);
-    int ok = on && lsize == CommBench::numproc;
+    int ok = on && lsize == CommBench::numproc && (!shared_device || on == 2);
     MPI_Allreduce(MPI_IN_PLACE, &ok, 1, MPI_INT, MPI_LAND, CommBench::comm_mpi);
+    if (on && !ok && shared_device && CommBench::myid == CommBench::printid)
+      std::printf("HiCCL: ranks share a GPU -- stream-ordered mode needs one GPU per rank; running host-driven "
+                  "(HICCL_STREAM_ORDERED=force overrides)\n");
     return ok != 0;
 #endif
   }

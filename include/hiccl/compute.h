@@ -1,13 +1,13 @@
 // include/hiccl/compute.h -- HiCCL::Compute<T>, the reduction compute stage.
 //
-// Same object contract as the reference (source/compute.h:80-258): add()
-// registers one compute on its owning rank (SPMD filter, compute.h:120),
+// Same object contract as the reference (source/compute.h:26-204): add()
+// registers one compute on its owning rank (SPMD filter, compute.h:66),
 // start() launches every registered compute, wait() blocks until they are
 // done, report()/measure() print the reference's tables.  The MI355X port
 // keeps all registered computes in ONE hiccl_reduce_plan and start() is a
 // single batched kernel launch on the process's compute stream (the
 // reference launches one reduce_kernel per compute on a stream of its own,
-// compute.h:141-160, and synchronises each, compute.h:161-171).
+// compute.h:87-106, and synchronises each, compute.h:107-117).
 //
 // Host port (HICCL_PORT_HOST, no GPU: config 1) runs the same in-order sum
 // with OpenMP on host memory, like the reference's no-PORT build
@@ -69,7 +69,7 @@ class Compute {
   Compute(const Compute &) = delete;
   Compute &operator=(const Compute &) = delete;
 
-  // compute.h:101-139.  Every rank calls add; the owning rank records.
+  // compute.h:47-85.  Every rank calls add; the owning rank records.
   void add(std::vector<T *> &in, T *out, size_t n, int compid) {
     if (CommBench::myid != compid) return;
     inputbuf.push_back(in);
@@ -92,7 +92,7 @@ class Compute {
 #endif
   }
 
-  // compute.h:141-160: nonblocking launch of all registered computes.
+  // compute.h:87-106: nonblocking launch of all registered computes.
   void start() {
     if (!numcomp) return;
 #ifndef HICCL_PORT_HOST
@@ -109,14 +109,22 @@ class Compute {
   }
 #endif
 
-  // compute.h:161-171
+  // Algorithmic bytes of one start(): sum of count * (n + 1) * sizeof(T)
+  // (the compute.h:197-203 accounting).
+  size_t bytes() const {
+    size_t b = 0;
+    for (int c = 0; c < numcomp; c++) b += count[c] * (inputbuf[c].size() + 1) * sizeof(T);
+    return b;
+  }
+
+  // compute.h:107-117
   void wait() {
 #ifndef HICCL_PORT_HOST
     if (numcomp) check(hiccl_reduce_plan_sync(plan), "plan_sync");
 #endif
   }
 
-  // compute.h:173-189
+  // compute.h:119-135
   void report() {
     std::vector<int> nc(CommBench::numproc), ni(CommBench::numproc);
     int numinput = 0;
@@ -130,7 +138,7 @@ class Compute {
     }
   }
 
-  // compute.h:191-250: time start()+wait() with barriers, MAX over ranks,
+  // compute.h:137-196: time start()+wait() with barriers, MAX over ranks,
   // price `count` elements (the caller's choice, as the reference does).
   void measure(int warmup, int numiter, size_t cnt) {
     report();
@@ -164,7 +172,7 @@ class Compute {
     roofline_bytes = 0;
   }
 
-  // compute.h:251-257: price reads + writes, sum over ranks.  Also prints
+  // compute.h:197-203: price reads + writes, sum over ranks.  Also prints
   // the per-GPU HBM roofline fraction: the busiest rank's algorithmic bytes
   // over the median time against the 8 TB/s MI355X peak.
   void measure(int warmup, int numiter) {

@@ -13,8 +13,11 @@
 //                  keep a step from overwriting bytes a peer still reads
 //   MPI            MPI_Isend/Irecv; device buffers staged through pinned
 //                  host memory (MPICH here is not GPU-aware)
-//   XCCL           RCCL point-to-point when built with HICCL_WITH_RCCL,
-//                  otherwise served as IPC
+//   XCCL           RCCL point-to-point (ncclSend/ncclRecv in one group per
+//                  step on the transport stream) when built with
+//                  HICCL_WITH_RCCL and every rank drives its own GPU
+//                  (RCCL refuses two ranks on one device); otherwise the
+//                  level runs on the IPC path and init() says so
 //   dummy          nothing
 //
 // Host port (HICCL_PORT_HOST, config 1: no GPU): buffers are host memory and
@@ -48,6 +51,8 @@
 #include <rccl/rccl.h>
 #endif
 #endif
+
+#include <unistd.h>
 
 namespace CommBench {
 
@@ -117,6 +122,62 @@ inline void init() {
 }
 
 #ifndef HICCL_PORT_HOST
+// True on every rank when two or more ranks of comm_mpi drive the same
+// device (same host, same PCI bus id): CommBench::init assigns devices
+// round-robin, so a node with more ranks than GPUs shares them.
+// Collective over comm_mpi.
+inline bool ranks_share_device() {
+  char key[192];
+  std::memset(key, 0, sizeof(key));
+  char host[96] = {0};
+  (void)gethostname(host, sizeof(host) - 1);
+  char bus[64] = {0};
+  hip_check(hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, mydevice), "hipDeviceGetPCIBusId");
+  std::snprintf(key, sizeof(key), "%s/%s", host, bus);
+  std::vector<char> all((size_t)numproc * sizeof(key));
+  mpi_check(MPI_Allgather(key, sizeof(key), MPI_CHAR, all.data(), sizeof(key), MPI_CHAR, comm_mpi),
+            "MPI_Allgather(device keys)");
+  std::vector<std::string> keys;
+  for (int r = 0; r < numproc; r++) keys.emplace_back(all.data() + (size_t)r * sizeof(key));
+  std::sort(keys.begin(), keys.end());
+  return std::adjacent_find(keys.begin(), keys.end()) != keys.end();
+}
+
+// ------------------------------------------------------------- RCCL ------
+// The XCCL library level: one RCCL communicator over comm_mpi, created by
+// xccl_setup() (collective) before any Comm<T> of an XCCL level is built.
+inline bool &xccl_on() {
+  static bool on = false;
+  return on;
+}
+#ifdef HICCL_WITH_RCCL
+inline ncclComm_t &xccl_comm() {
+  static ncclComm_t c = nullptr;
+  return c;
+}
+inline void nccl_check(ncclResult_t e, const char *what) {
+  if (e != ncclSuccess) die(what, ncclGetErrorString(e));
+}
+#endif
+// Collective.  Returns whether XCCL levels run on RCCL; otherwise they run
+// on the IPC path (no RCCL in this build, or ranks sharing a device).
+inline bool xccl_setup(bool shared_device) {
+#ifdef HICCL_WITH_RCCL
+  if (xccl_on()) return true;
+  if (shared_device) return false;
+  ncclUniqueId id;
+  if (myid == 0) nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  mpi_check(MPI_Bcast(&id, sizeof(id), MPI_BYTE, 0, comm_mpi), "MPI_Bcast(nccl id)");
+  setup_gpu();
+  nccl_check(ncclCommInitRank(&xccl_comm(), numproc, id, myid), "ncclCommInitRank");
+  xccl_on() = true;
+  return true;
+#else
+  (void)shared_device;
+  return false;
+#endif
+}
+
 // One transport stream per process: the steps of a pipeline run one after
 // the other on a rank, so every Comm shares it (the reference creates
 // streams per object; hundreds of them oversubscribe the hardware queues).
@@ -268,9 +329,14 @@ struct FlagSpace {
   uint32_t *err = nullptr;
 
   // Collective over comm_mpi.
+  // The flags are uncached device memory (hipDeviceMallocUncached): a peer
+  // GPU writes them over xGMI while a kernel here spins on them, and plain
+  // (coarse-grained) hipMalloc memory is only coherent at dispatch
+  // boundaries -- a line held in this device's L2 could hide the write.
   void create(size_t n) {
     nflags = std::max<size_t>(n, 1);
-    hip_check(hipMalloc((void **)&local, nflags * sizeof(uint32_t)), "hipMalloc(flags)");
+    hip_check(hipExtMallocWithFlags((void **)&local, nflags * sizeof(uint32_t), hipDeviceMallocUncached),
+              "hipExtMallocWithFlags(flags, uncached)");
     hip_check(hipMemset(local, 0, nflags * sizeof(uint32_t)), "hipMemset(flags)");
     hip_check(hipHostMalloc((void **)&err, sizeof(uint32_t), hipHostMallocCoherent), "hipHostMalloc(err)");
     *err = 0;
@@ -326,6 +392,8 @@ inline void signal_wait(const std::vector<uint32_t *> &sig, const std::vector<ui
 // mode: the same two signals are device flags (ready in the mover's
 // FlagSpace slot 2*(base+j), done in the owner's slot 2*(base+j)+1), set and
 // awaited by hiccl_signal_wait on the rank's stream around the copies.
+constexpr int kDoneTag = 16000;
+
 template <typename T>
 class Comm {
  public:
@@ -338,7 +406,7 @@ class Comm {
     if (this->lib != dummy) this->lib = MPI;
 #else
     streamed = stream_ordered;
-    if (this->lib == XCCL) this->lib = IPC;  // served over the same xGMI path (see header comment)
+    if (this->lib == XCCL && !xccl_on()) this->lib = IPC;  // no RCCL (see xccl_setup): the xGMI IPC path
     if (streamed && this->lib == MPI) this->lib = IPC;  // one node: move device bytes directly
     stream = transport_stream();
 #endif
@@ -373,10 +441,12 @@ class Comm {
     x.count = count;
     x.sendid = sendid;
     x.recvid = recvid;
-    x.tag = (int)(xfers.size() % 30000);
+    // tags stay below MPI's guaranteed MPI_TAG_UB (32767): the done token of
+    // a transfer uses tag + kDoneTag
+    x.tag = (int)(xfers.size() % kDoneTag);
     if (myid == sendid) numsend++;
     if (myid == recvid) numrecv++;
-    if (lib == dummy || count == 0) {
+    if (lib == dummy || count == 0 || lib == XCCL) {  // XCCL: RCCL needs no registration
       xfers.push_back(x);
       return;
     }
@@ -421,7 +491,8 @@ class Comm {
     tail_wait.clear();
     for (size_t j = 0; j < xfers.size(); j++) {
       const Xfer &x = xfers[j];
-      if (lib == dummy || x.count == 0 || x.sendid == x.recvid) continue;
+      // XCCL: RCCL orders its sends and receives on the stream itself
+      if (lib == dummy || lib == XCCL || x.count == 0 || x.sendid == x.recvid) continue;
       const int owner = owner_of(x), mover = mover_of(x);
       const size_t ready = 2 * (base + j), done = ready + 1;
       if (myid == owner) {
@@ -440,6 +511,10 @@ class Comm {
   // done tokens of fused transfers follow the step's compute: enqueue_tail.
   void enqueue(hipStream_t s) {
     ++epoch;
+    if (lib == XCCL) {
+      xccl_group(s);
+      return;
+    }
     signal_wait(pre_sig, pre_wait, sig_epoch(), graph_epoch, flags->err, s);
     launch_copies(s);
     signal_wait(post_sig, post_wait, sig_epoch(), graph_epoch, flags->err, s);
@@ -469,6 +544,10 @@ class Comm {
       if (!flags) die("transport", "stream-ordered Comm used before bind()");
       enqueue(stream);
       enqueue_tail(stream);  // standalone use (measure): no compute in between
+      return;
+    }
+    if (lib == XCCL) {
+      xccl_group(stream);
       return;
     }
     build_plans();
@@ -519,9 +598,9 @@ class Comm {
         post(MPI_Isend(nullptr, 0, MPI_BYTE, peer, x.tag, comm_mpi, next()));  // ready
         if (x.fused) {
           tail_reqs.emplace_back();  // done: after the reader's compute, in finish()
-          post(MPI_Irecv(nullptr, 0, MPI_BYTE, peer, x.tag + 30000, comm_mpi, &tail_reqs.back()));
+          post(MPI_Irecv(nullptr, 0, MPI_BYTE, peer, x.tag + kDoneTag, comm_mpi, &tail_reqs.back()));
         } else {
-          post(MPI_Irecv(nullptr, 0, MPI_BYTE, peer, x.tag + 30000, comm_mpi, next()));  // done
+          post(MPI_Irecv(nullptr, 0, MPI_BYTE, peer, x.tag + kDoneTag, comm_mpi, next()));  // done
         }
       }
 #endif
@@ -531,7 +610,7 @@ class Comm {
   void wait() {
 #ifndef HICCL_PORT_HOST
     setup_gpu();
-    if (streamed) {
+    if (streamed || lib == XCCL) {
       hip_check(hipStreamSynchronize(stream), "transport stream sync");
       if (flags && *flags->err) die("transport", "stream-ordered signal timed out (peer never signalled)");
       return;
@@ -543,7 +622,7 @@ class Comm {
     for (auto &m : movers) {
       const Xfer &x = *m.x;
       const int peer = myid == x.sendid ? x.recvid : x.sendid;
-      post(MPI_Isend(nullptr, 0, MPI_BYTE, peer, x.tag + 30000, comm_mpi, next()));  // done
+      post(MPI_Isend(nullptr, 0, MPI_BYTE, peer, x.tag + kDoneTag, comm_mpi, next()));  // done
     }
 #endif
     if (!reqs.empty()) mpi_check(MPI_Waitall((int)reqs.size(), reqs.data(), MPI_STATUSES_IGNORE), "MPI_Waitall");
@@ -566,7 +645,7 @@ class Comm {
     for (auto &m : readers) {
       const int peer = m.x->sendid;
       tail_reqs.emplace_back();
-      post(MPI_Isend(nullptr, 0, MPI_BYTE, peer, m.x->tag + 30000, comm_mpi, &tail_reqs.back()));
+      post(MPI_Isend(nullptr, 0, MPI_BYTE, peer, m.x->tag + kDoneTag, comm_mpi, &tail_reqs.back()));
     }
     if (!tail_reqs.empty())
       mpi_check(MPI_Waitall((int)tail_reqs.size(), tail_reqs.data(), MPI_STATUSES_IGNORE), "MPI_Waitall(done)");
@@ -661,6 +740,30 @@ class Comm {
     build_plans();
     if (moveplan) launch_plan(moveplan, s, "IPC moves");
     if (selfplan) launch_plan(selfplan, s, "self copies");
+  }
+
+  // XCCL level: this rank's self copies (one batched kernel) and its sends
+  // and receives as one RCCL group on `s`, in registration order (every
+  // rank registers the same transfers in the same order, so each pair's
+  // sends and receives match).
+  void xccl_group(hipStream_t s) {
+    build_plans();
+    if (selfplan) launch_plan(selfplan, s, "self copies");
+#ifdef HICCL_WITH_RCCL
+    bool any = false;
+    for (const Xfer &x : xfers)
+      if (x.count && x.sendid != x.recvid && (myid == x.sendid || myid == x.recvid)) any = true;
+    if (!any) return;
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (const Xfer &x : xfers) {
+      if (!x.count || x.sendid == x.recvid) continue;
+      if (myid == x.sendid)
+        nccl_check(ncclSend(x.src, x.count * sizeof(T), ncclUint8, x.recvid, xccl_comm(), s), "ncclSend");
+      if (myid == x.recvid)
+        nccl_check(ncclRecv(x.dst, x.count * sizeof(T), ncclUint8, x.sendid, xccl_comm(), s), "ncclRecv");
+    }
+    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+#endif
   }
 #endif
 

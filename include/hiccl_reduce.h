@@ -72,10 +72,12 @@ typedef enum {
  *            (one per device and stream, reset by the launch itself):
  *            faster-served workgroups do more units, the tail is one ticket.
  *   AUTO     DYNAMIC for the TILE engine with >= 5 inputs and >= 32 tickets
- *            per workgroup, STATIC otherwise and always during stream
- *            capture.  A forced DYNAMIC still needs >= 32 tickets per
- *            workgroup.
- * Plans use AUTO. */
+ *            per workgroup, STATIC otherwise.
+ * Always STATIC during stream capture (a replayed graph must not share a
+ * stream's counter) and on hipStreamPerThread (one handle value, a different
+ * stream per host thread).  A forced DYNAMIC still needs >= 32 tickets per
+ * workgroup.  Plans take the schedule of hiccl_reduce_plan_set_config
+ * (default AUTO). */
 typedef enum {
   HICCL_SCHED_AUTO = 0,
   HICCL_SCHED_STATIC = 1,
@@ -93,8 +95,8 @@ int hiccl_version(void);
 
 /* ----------------------------------------------------------------------
  * One-shot reduction.  Replaces one registered compute of the reference's
- * Compute<T> being launched: compute.h:145 (launch of reduce_kernel with
- * the device pointer table built at compute.h:124-126).
+ * Compute<T> being launched: compute.h:90-91 (launch of reduce_kernel with
+ * the device pointer table built at compute.h:70-72).
  *
  *   in     HOST array of n DEVICE pointers, in summation order (the order
  *          reduce.h:134-169 emits: ascending rank).  Copied at call time;
@@ -113,7 +115,11 @@ int hiccl_reduce_bf16(uint16_t *out, const uint16_t *const *in, int n, size_t co
                       void *stream);
 
 /* Tuning knobs of the single-compute kernel.  Zero fields mean "default".
- * With engine AUTO, a non-zero block or unroll selects the TILE engine. */
+ * With engine AUTO, a non-zero block or unroll selects the TILE engine.
+ * With n > 64 inputs the call runs on the plan kernel (pointer table in
+ * device memory), which has fewer shapes (hiccl_reduce_plan_set_config): a
+ * shape it lacks is an error, never silently replaced; such a call cannot
+ * be captured into a graph (hipErrorStreamCaptureUnsupported). */
 typedef struct {
   int block;         /* threads per workgroup: TILE 256 or 512; PHASE 256, 512 or 1024 */
   int unroll;        /* 16-byte packets per input per lane per tile: TILE 1, 2 or 4;
@@ -137,23 +143,23 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
  * Persistent plan: the C-ABI counterpart of the reference's Compute<T>
  * (compute.h:26-204).  A plan holds any number of registered computes and
  * launches ALL of them in ONE kernel (one launch per pipeline step instead
- * of one launch + one stream per compute, compute.h:141-159).
+ * of one launch + one stream per compute, compute.h:87-106).
  *
- *   create   compute.h:26 (object) -- binds `device`.
- *   add      compute.h:101-139 add(inputbuf, outputbuf, count, compid):
+ *   create   compute.h:26-45 (object) -- binds `device`.
+ *   add      compute.h:47-85 add(inputbuf, outputbuf, count, compid):
  *            records one compute; `in` is a HOST array of n DEVICE
  *            pointers, copied.  (The reference's SPMD "only if myid ==
- *            compid" filter is applied by the C++ caller.)
- *   launch   compute.h:141-160 start(): one batched kernel on `stream`
+ *            compid" filter, compute.h:66, is applied by the C++ caller.)
+ *   launch   compute.h:87-106 start(): one batched kernel on `stream`
  *            (NULL = the default stream, as everywhere in this ABI; the
  *            plan's own stream -- the reference creates one per compute,
- *            compute.h:131-132 -- is hiccl_reduce_plan_stream()).  The first
- *            launch after an add uploads the descriptor table (synchronous,
- *            once).
- *   sync     compute.h:161-171 wait(): blocks until the plan's last launch
+ *            compute.h:76-78 -- is hiccl_reduce_plan_stream()).  The first
+ *            launch after an add or a config change uploads the descriptor
+ *            table (synchronous, once; refused inside a stream capture).
+ *   sync     compute.h:107-117 wait(): blocks until the plan's last launch
  *            has completed.
  *   destroy  frees the plan's device tables and stream (the reference leaks
- *            them, compute.h:124-137).
+ *            them, compute.h:70-82).
  * Threading: launch/sync may be called from a different host thread than
  * create/add (Comm::start's pthread, comm.h:214-224); each entry binds the
  * plan's device.  Not reentrant per plan; distinct plans are independent.
@@ -165,15 +171,22 @@ int hiccl_reduce_plan_set_acc(hiccl_reduce_plan_t *plan, int acc);
 /* Engine for the plan's launches (hiccl_engine_t; default AUTO, decided from
  * the total packets of all computes at the first launch after an add). */
 int hiccl_reduce_plan_set_engine(hiccl_reduce_plan_t *plan, int engine);
+/* Kernel configuration of the plan's launches (NULL = all defaults; replaces
+ * earlier set_engine / set_acc choices).  Honoured: engine, schedule, grab,
+ * blocks_per_cu, grid, acc, and the TILE shape block 256 x unroll 4 (f32 and
+ * bf16 also unroll 1 or 2); PHASE runs its default shape; loads and stores
+ * are nt.  Anything else is refused with hipErrorInvalidValue -- no field is
+ * silently ignored. */
+int hiccl_reduce_plan_set_config(hiccl_reduce_plan_t *plan, const hiccl_reduce_config_t *cfg);
 /* The engine the last upload resolved to (TILE before the first launch). */
 int hiccl_reduce_plan_engine(const hiccl_reduce_plan_t *plan);
 int hiccl_reduce_plan_add(hiccl_reduce_plan_t *plan, void *out, const void *const *in, int n,
                           size_t count);
 int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *plan, void *stream);
 /* Reference structure, for measurement: one kernel per compute, each on
- * the given stream (compute.h:141-145 launches one kernel per compute) --
- * each one a one-shot hiccl_reduce_ex with the plan's acc and engine
- * request (AUTO decides per compute). */
+ * the given stream (compute.h:88-91 launches one kernel per compute) --
+ * each one a one-shot hiccl_reduce_ex with the plan's configuration (AUTO
+ * decides per compute). */
 int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *plan, void *stream);
 int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *plan);
 /* The plan's own non-blocking stream (a hipStream_t), created on the first
@@ -181,7 +194,7 @@ int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *plan);
 void *hiccl_reduce_plan_stream(hiccl_reduce_plan_t *plan);
 int hiccl_reduce_plan_numcomp(const hiccl_reduce_plan_t *plan);
 /* Sum over computes of count * (n + 1) * sizeof(T): the bytes the reference's
- * measure(warmup, numiter) overload (compute.h:251-257) prices. */
+ * measure(warmup, numiter) overload (compute.h:197-203) prices. */
 size_t hiccl_reduce_plan_bytes(const hiccl_reduce_plan_t *plan);
 void hiccl_reduce_plan_destroy(hiccl_reduce_plan_t *plan);
 

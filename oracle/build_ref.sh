@@ -53,11 +53,17 @@ if [ -f "$DRV" ] && [ -f "$MPI_INC/mpi.h" ]; then
   ( cd "$ROOT/include/hiccl" && g++ -std=c++17 -O2 -fopenmp -DHICCL_PORT_HOST -I"$MPI_INC" \
       -x c++ - -x none -o "$OUTDIR/collectives_main_host" $MPI_LINK < "$DRV" )
   echo "build_ref: built $OUTDIR/collectives_main_host from $DRV against include/hiccl.h"
-  if [ -f "$ROOT/hiccl_amd/libhiccl_reduce.so" ]; then
-    ( cd "$ROOT/include/hiccl" && g++ -std=c++17 -O2 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -I"$MPI_INC" \
-        -x c++ - -x none -o "$OUTDIR/collectives_main_hip" \
-        -L"$ROOT/hiccl_amd" -lhiccl_reduce -Wl,-rpath,'$ORIGIN/../../hiccl_amd' \
-        -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib $MPI_LINK < "$DRV" )
-    echo "build_ref: built $OUTDIR/collectives_main_hip from $DRV against include/hiccl.h"
-  fi
+  # the HIP port needs the product library: a missing one is a build-order
+  # error, never a silent skip (tests/test_reference_driver.py fails when the
+  # stamp below exists and a driver does not)
+  [ -f "$ROOT/hiccl_amd/libhiccl_reduce.so" ] || {
+    echo "build_ref: hiccl_amd/libhiccl_reduce.so missing -- build it first (make)" >&2; exit 1; }
+  ( cd "$ROOT/include/hiccl" && g++ -std=c++17 -O2 -D__HIP_PLATFORM_AMD__ -DHICCL_WITH_RCCL -I/opt/rocm/include -I"$MPI_INC" \
+      -x c++ - -x none -o "$OUTDIR/collectives_main_hip" \
+      -L"$ROOT/hiccl_amd" -lhiccl_reduce -Wl,-rpath,'$ORIGIN/../../hiccl_amd' \
+      -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib $MPI_LINK < "$DRV" )
+  echo "build_ref: built $OUTDIR/collectives_main_hip from $DRV against include/hiccl.h"
+  # stamp: this tree was built where the reference was present, so every
+  # reference-built artefact must exist wherever the tree is tested
+  echo "reference: $REF" > "$OUTDIR/BUILT_FROM_REFERENCE"
 fi

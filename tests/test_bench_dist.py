@@ -58,3 +58,66 @@ def test_single_rank_no_launcher():
     sys.path.insert(0, ROOT)
     import bench
     assert bench.whole_job_gbps(1, 9 << 30, 20, 0.0344) == pytest.approx(9 * 2**30 * 20 / 0.0344 / 1e9)
+
+
+def _c5_rank(rank, world, port, q):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import argparse
+
+    import bench
+    # the config-5 leg runs before Dist (no GPU touched); on a box without one
+    # GPU per rank it is skipped, and every rank receives rank 0's verdict
+    res = bench.c5_leg(argparse.Namespace(c5_log2count=10, c5_iters=1))
+    d = bench.Dist(world)  # reuses the control plane the leg started
+    d.barrier()
+    q.put((rank, res, d.backend))
+    d.close()
+
+
+def test_c5_leg_broadcasts_rank0_result():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_c5_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == res[1][1]
+    assert "skipped" in res[0][1] and "one GPU per rank" in res[0][1]["skipped"]
+    assert all(r[2] == "gloo" for r in res)
+
+
+def test_cpu_leg_full_bucket_parity(tmp_path):
+    """bench.py's CPU baseline child: times the reference's reduce_kernel and
+    compares a GPU output file word for word (here: the oracle's own output,
+    then the same with one word flipped)."""
+    import json
+    import subprocess
+
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from conftest import Oracle, _build_oracle
+    _build_oracle()
+    ora = Oracle()
+    n, log2c = 3, 16
+    exp = ora.reduce(list(ora.fill(n, 1 << log2c, 1234)))
+    good = tmp_path / "good.f32"
+    exp.tofile(good)
+    bad = exp.copy()
+    bad.view(np.uint32)[777] ^= 1
+    badf = tmp_path / "bad.f32"
+    bad.tofile(badf)
+    env = dict(os.environ, OMP_NUM_THREADS="2", OMP_PROC_BIND="spread")
+    for path, ok, mism in ((good, True, 0), (badf, False, 1)):
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-leg", "--n", str(n),
+                            "--log2count", str(log2c), "--cpu-budget", "0.2", "--expect-file", str(path)],
+                           capture_output=True, text=True, env=env, timeout=300)
+        assert p.returncode == 0, p.stderr[-2000:]
+        r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+        assert r["parity_full"]["ok"] is ok and r["parity_full"]["mismatches"] == mism
+        assert r["threads"] == 2 and "OMP_PROC_BIND=spread" in r["sample"]

@@ -28,12 +28,18 @@ HIP = os.path.join(ROOT, "build", "collectives_hip")
 HIP_F32 = os.path.join(ROOT, "build", "collectives_hip_f32")
 
 
-def mpirun(np_, exe, args, timeout=180, streamed=True, fused=False, engine="auto", graph=False, repeat=1):
+def mpirun(np_, exe, args, timeout=180, streamed=True, fused=False, engine="auto", graph=False, repeat=1,
+           stream_env=None, queues=True):
+    """streamed: HICCL_STREAM_ORDERED=force -- every rank here shares the box's
+    one GPU, where the library would otherwise fall back to host-driven mode
+    (tested by test_shared_device_falls_back_to_host_driven)."""
     assert np_ <= 8
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED="1" if streamed else "0",
+    if stream_env is None:
+        stream_env = "force" if streamed else "0"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED=stream_env,
                HICCL_FUSED_GATHER="1" if fused else "0", HICCL_SIGNAL_TIMEOUT="10", HICCL_ENGINE=engine,
                HICCL_GRAPH="1" if graph else "0", HICCL_DRIVER_REPEAT=str(repeat))
-    if np_ > 4:
+    if np_ > 4 and queues:
         # every rank on the box's one GPU: 8 processes x 4 hardware queues
         # oversubscribe the device's queue slots, and a spinning stream-ordered
         # wait can then outlast its timeout while the peer's queue is not
@@ -129,3 +135,42 @@ def test_readme_api_example(np_, streamed):
     rc, out = mpirun(np_, os.path.join(ROOT, "build", "readme_example_hip"), [250000, 3], streamed=streamed)
     assert rc == 0, out[-3000:]
     assert "README all-reduce: PASSED" in out
+
+
+@pytest.mark.parametrize("pattern", [8, 7])
+def test_shared_device_falls_back_to_host_driven(pattern):
+    """8 ranks on one GPU asking for stream-ordered mode (HICCL_STREAM_ORDERED=1)
+    at HIP's default hardware-queue count: init() detects the shared device
+    (PCI bus id per rank) and runs host-driven, so nothing spins while a
+    peer's queue is unmapped -- the known-answer test passes without any
+    GPU_MAX_HW_QUEUES override."""
+    rc, out = mpirun(8, HIP, [pattern, 4099, 1, 1, 3, 1, 2, "1,4,2", "mpi,ipc,ipc"], stream_env="1", queues=False)
+    assert rc == 0, out[-3000:]
+    assert "PASSED!" in out
+    assert "ranks share a GPU" in out and "host-driven" in out
+
+
+def test_xccl_level_shared_device_uses_ipc_path():
+    """An XCCL level with ranks sharing the one GPU: RCCL refuses two ranks on
+    one device, so the level runs on the IPC path (said at init) and the
+    known-answer test passes."""
+    rc, out = mpirun(4, HIP, [8, 4099, 1, 1, 3, 0, 0, "2,2", "ipc,xccl"], streamed=False)
+    assert rc == 0, out[-3000:]
+    assert "PASSED!" in out
+    assert "XCCL levels run on the IPC path" in out
+
+
+def _ngpus():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_ngpus() < 2, reason="RCCL point-to-point needs one GPU per rank (>= 2 GPUs)")
+@pytest.mark.parametrize("streamed", [False, True], ids=["host", "stream"])
+def test_xccl_level_on_rccl(streamed):
+    """One GPU per rank: the XCCL level moves its bytes with ncclSend/ncclRecv."""
+    n = min(_ngpus(), 8)
+    rc, out = mpirun(n, HIP, [8, 4099, 1, 1, 3, 0, 0, str(n), "xccl"], streamed=streamed,
+                     stream_env="1" if streamed else "0")
+    assert rc == 0, out[-3000:]
+    assert "PASSED!" in out and "XCCL on RCCL" in out

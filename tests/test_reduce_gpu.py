@@ -349,7 +349,7 @@ def _plan_case(oracle, each, engine=hiccl_amd.HICCL_ENGINE_AUTO):
         comp.add(ins, (ob, 1), count, compid=0)
         outs.append((ob, count))
         expected.append(oracle.reduce(list(x)))
-    comp.add([(keep[0], 0)], (keep[0], 0), 1, compid=3)  # not mine: ignored (compute.h:120)
+    comp.add([(keep[0], 0)], (keep[0], 0), 1, compid=3)  # not mine: ignored (compute.h:66)
     assert comp.numcomp == 37
     comp.start(each=each)
     comp.wait()

@@ -19,6 +19,18 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF_HOST = os.path.join(ROOT, "oracle", "_ref", "collectives_main_host")
 REF_HIP = os.path.join(ROOT, "oracle", "_ref", "collectives_main_hip")
+# written by oracle/build_ref.sh when /root/reference was present at build
+# time: from then on a missing driver is a build failure, not a skip
+STAMP = os.path.join(ROOT, "oracle", "_ref", "BUILT_FROM_REFERENCE")
+
+
+def need(exe):
+    if os.path.exists(exe):
+        return
+    if os.path.exists(STAMP) or os.path.isdir("/root/reference/collectives"):
+        pytest.fail(f"{exe} missing although the tree was built with the reference present "
+                    "(oracle/build_ref.sh): build order broken")
+    pytest.skip("reference driver not built (tree built without /root/reference)")
 MPIRUN = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
 NAMES = {1: "GATHER", 2: "SCATTER", 3: "BCAST", 4: "REDUCE", 5: "ALL-TO-ALL", 6: "ALL-GATHER",
          7: "REDUCE-SCATTER", 8: "ALL-REDUCE"}
@@ -32,20 +44,25 @@ def run(exe, np_, args, env_extra=None, timeout=240):
     return p.returncode, p.stdout + p.stderr
 
 
-@pytest.mark.skipif(not os.path.exists(REF_HOST), reason="reference driver not built (needs /root/reference)")
 @pytest.mark.parametrize("np_,args", [(8, [1000, 1, 1, 4, 1, 2]), (8, [999, 2, 2, 3, 0, 1]),
                                       (16, [257, 1, 1, 2, 0, 1])])
 @pytest.mark.parametrize("pattern", range(1, 9))
 def test_reference_driver_host(pattern, np_, args):
+    need(REF_HOST)
     rc, out = run(REF_HOST, np_, [pattern] + args)
     assert f"VERIFY {NAMES[pattern]} ROOT = 0: PASSED!" in out, out[-3000:]
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(not os.path.exists(REF_HIP), reason="reference driver not built (needs /root/reference)")
 @pytest.mark.parametrize("streamed", ["0", "1"], ids=["host", "stream"])
 @pytest.mark.parametrize("pattern", [7, 8])
 def test_reference_driver_gpu(pattern, streamed):
-    # 8 processes time-share one GPU here: keep the driver's own measure loops minimal
+    """HIP port; 8 processes time-share the box's one GPU (the driver's
+    hard-coded {4,4,2} needs 32 ranks for its levels to differ; 8 run it with
+    the ring/tree logic of the same code).  With HICCL_STREAM_ORDERED=1 on a
+    shared device the library runs host-driven (Comm::init detects it); the
+    KAT must pass either way, at the default hardware-queue count."""
+    need(REF_HIP)
+    # keep the driver's own measure loops minimal
     rc, out = run(REF_HIP, 8, [pattern, 4099, 1, 1, 4, 0, 1], {"HICCL_STREAM_ORDERED": streamed})
     assert f"VERIFY {NAMES[pattern]} ROOT = 0: PASSED!" in out, out[-3000:]
