@@ -179,6 +179,12 @@ class Compute:
         fn = L.lib().hiccl_reduce_plan_launch_each if each else L.lib().hiccl_reduce_plan_launch
         L.check(fn(self._plan, s), "plan_launch")
 
+    def enqueue(self, stream=None):
+        """Launch on ``stream`` (default torch's current stream) without the
+        completion event :meth:`wait` uses (hiccl_reduce_plan_enqueue): for
+        stream-ordered pipelines that synchronise the stream themselves."""
+        L.check(L.lib().hiccl_reduce_plan_enqueue(self._plan, _stream_handle(stream)), "plan_enqueue")
+
     def wait(self):
         L.check(L.lib().hiccl_reduce_plan_sync(self._plan), "plan_sync")
 

@@ -1256,7 +1256,7 @@ struct hiccl_reduce_plan {
   PlanArgs args;            // pointers into d_block
   uint64_t total_tiles = 0;
   hipStream_t own = nullptr;
-  hipEvent_t done = nullptr;
+  hipStream_t last = nullptr;  // stream of the last launch (plan_sync synchronises it)
   bool launched = false;
 };
 
@@ -1301,7 +1301,7 @@ int plan_upload(hiccl_reduce_plan *p, hipStream_t s) {
     return fail(hipErrorStreamCaptureUnsupported,
                 "plan: the first launch after an add or a config change uploads the plan and cannot be captured");
   if (p->d_block) {
-    if (p->launched) (void)hipEventSynchronize(p->done);  // a running launch still reads it
+    if (p->launched) (void)hipStreamSynchronize(p->last);  // a running launch still reads it
     (void)hipFree(p->d_block);
     p->d_block = nullptr;
   }
@@ -1437,10 +1437,6 @@ int hiccl_reduce_plan_create(hiccl_reduce_plan_t **plan, int dtype, int device) 
   p->esz = esize(dtype);
   // the plan's own stream is created on first request (hiccl_reduce_plan_stream):
   // callers that launch on a shared stream never pay for one
-  if (int e = check_hip(hipEventCreateWithFlags(&p->done, hipEventDisableTiming), "plan_create: event")) {
-    delete p;
-    return e;
-  }
   *plan = p;
   return 0;
 }
@@ -1512,18 +1508,25 @@ int hiccl_reduce_plan_add(hiccl_reduce_plan_t *p, void *out, const void *const *
   return 0;
 }
 
-int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *p, void *stream) {
-  if (!p) return fail(hipErrorInvalidValue, "plan_launch: plan is NULL");
-  if (int e = check_hip(hipSetDevice(p->device), "plan_launch: hipSetDevice")) return e;
+int hiccl_reduce_plan_enqueue(hiccl_reduce_plan_t *p, void *stream) {
+  if (!p) return fail(hipErrorInvalidValue, "plan_enqueue: plan is NULL");
+  if (int e = check_hip(hipSetDevice(p->device), "plan_enqueue: hipSetDevice")) return e;
   if (p->comps.empty()) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (int e = plan_upload(p, s)) return e;
-  if (int e = plan_kernel(p, s)) return e;
+  return plan_kernel(p, s);
+}
+
+int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *p, void *stream) {
+  if (int e = hiccl_reduce_plan_enqueue(p, stream)) return e;
+  if (p->comps.empty()) return 0;
+  hipStream_t s = (hipStream_t)stream;
   // a capturing stream gets no completion event (plan_sync does not apply
   // to graph replays: synchronise the stream the graph runs on)
   if (capturing(s, false)) return 0;
   p->launched = true;
-  return check_hip(hipEventRecord(p->done, s), "plan_launch: event");
+  p->last = s;
+  return 0;
 }
 
 int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *p, void *stream) {
@@ -1536,14 +1539,18 @@ int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *p, void *stream) {
     if (int e = hiccl_reduce_ex(p->dtype, c.out, c.in.data(), (int)c.in.size(), c.count, stream, &p->req))
       return e;
   p->launched = true;
-  return check_hip(hipEventRecord(p->done, (hipStream_t)stream), "plan_launch_each: event");
+  p->last = (hipStream_t)stream;
+  return 0;
 }
 
 int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *p) {
   if (!p) return fail(hipErrorInvalidValue, "plan_sync: plan is NULL");
   if (!p->launched) return 0;
   if (int e = check_hip(hipSetDevice(p->device), "plan_sync: hipSetDevice")) return e;
-  return check_hip(hipEventSynchronize(p->done), "plan_sync");
+  // the reference's wait(): hipStreamSynchronize of the compute's stream
+  // (compute.h:107-117) -- no completion event per launch (an event record
+  // after every kernel costs the queue ~3 us per step on MI355X)
+  return check_hip(hipStreamSynchronize(p->last), "plan_sync");
 }
 
 int hiccl_reduce_plan_numcomp(const hiccl_reduce_plan_t *p) { return p ? (int)p->comps.size() : 0; }
@@ -1567,9 +1574,8 @@ size_t hiccl_reduce_plan_bytes(const hiccl_reduce_plan_t *p) {
 void hiccl_reduce_plan_destroy(hiccl_reduce_plan_t *p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
-  if (p->launched) (void)hipEventSynchronize(p->done);
+  if (p->launched) (void)hipStreamSynchronize(p->last);
   if (p->d_block) (void)hipFree(p->d_block);
-  if (p->done) (void)hipEventDestroy(p->done);
   if (p->own) (void)hipStreamDestroy(p->own);
   delete p;
 }

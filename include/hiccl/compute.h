@@ -17,7 +17,9 @@
 #define HICCL_COMPUTE_H
 
 #include <algorithm>
+#include <cstdint>
 #include <cstdio>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -29,6 +31,39 @@
 
 namespace HiCCL {
 
+// bfloat16 storage type for Comm<bf16> / Compute<bf16>.  The arithmetic is
+// the reference's `T acc = 0; acc += x` (compute.h:7-9) with T = bf16: an
+// f32 add rounded to nearest-even bf16 after every add -- the host port
+// below and the GPU kernels (HICCL_BFLOAT16, HICCL_ACC_NATIVE) give the same
+// bits.  Only this type maps to HICCL_BFLOAT16: other 2-byte types
+// (int16_t, uint16_t) have no reduction here and fail to compile.
+struct bf16 {
+  uint16_t bits = 0;
+  bf16() = default;
+  bf16(int v) : bits(round((float)v)) {}  // T acc = 0
+  explicit bf16(float f) : bits(round(f)) {}
+  explicit operator float() const {
+    uint32_t w = (uint32_t)bits << 16;
+    float f;
+    std::memcpy(&f, &w, 4);
+    return f;
+  }
+  bf16 &operator+=(bf16 o) {
+    bits = round((float)*this + (float)o);
+    return *this;
+  }
+  bool operator==(bf16 o) const { return bits == o.bits; }
+  bool operator!=(bf16 o) const { return bits != o.bits; }
+  static uint16_t round(float f) {  // round to nearest even; NaN stays NaN
+    uint32_t w;
+    std::memcpy(&w, &f, 4);
+    if ((w & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((w >> 16) | 0x40);
+    w += 0x7fffu + ((w >> 16) & 1u);
+    return (uint16_t)(w >> 16);
+  }
+};
+static_assert(sizeof(bf16) == 2, "bf16 storage");
+
 // T -> hiccl_dtype_t
 template <typename T>
 constexpr int dtype_of() {
@@ -36,7 +71,7 @@ constexpr int dtype_of() {
   else if constexpr (std::is_same<T, double>::value) return 1;
   else if constexpr (std::is_integral<T>::value && sizeof(T) == 8) return 3;
   else if constexpr (std::is_integral<T>::value && sizeof(T) == 4) return 4;
-  else if constexpr (sizeof(T) == 2) return 2;  // bf16 storage type
+  else if constexpr (std::is_same<T, bf16>::value) return 2;
   else return -1;
 }
 
@@ -105,7 +140,7 @@ class Compute {
 #ifndef HICCL_PORT_HOST
   // Stream-ordered execution: enqueue the step's batched kernel on `s`.
   void launch(hipStream_t s) {
-    if (numcomp) check(hiccl_reduce_plan_launch(plan, s), "plan_launch");
+    if (numcomp) check(hiccl_reduce_plan_enqueue(plan, s), "plan_enqueue");  // the caller syncs the stream
   }
 #endif
 

@@ -732,8 +732,10 @@ class Comm {
     }
   }
 
+  // the transport synchronises its stream (or orders it by flags), never a
+  // plan's completion event: enqueue without one
   static void launch_plan(hiccl_reduce_plan_t *p, hipStream_t s, const char *what) {
-    if (hiccl_reduce_plan_launch(p, s)) die(what, hiccl_last_error());
+    if (hiccl_reduce_plan_enqueue(p, s)) die(what, hiccl_last_error());
   }
 
   void launch_copies(hipStream_t s) {

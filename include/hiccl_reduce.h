@@ -156,8 +156,10 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
  *            compute.h:76-78 -- is hiccl_reduce_plan_stream()).  The first
  *            launch after an add or a config change uploads the descriptor
  *            table (synchronous, once; refused inside a stream capture).
- *   sync     compute.h:107-117 wait(): blocks until the plan's last launch
- *            has completed.
+ *   sync     compute.h:107-117 wait(): hipStreamSynchronize of the stream
+ *            of the plan's last launch (as the reference synchronises each
+ *            compute's stream) -- that stream must still exist.  No event is
+ *            recorded per launch.
  *   destroy  frees the plan's device tables and stream (the reference leaks
  *            them, compute.h:70-82).
  * Threading: launch/sync may be called from a different host thread than
@@ -183,6 +185,10 @@ int hiccl_reduce_plan_engine(const hiccl_reduce_plan_t *plan);
 int hiccl_reduce_plan_add(hiccl_reduce_plan_t *plan, void *out, const void *const *in, int n,
                           size_t count);
 int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *plan, void *stream);
+/* launch without remembering the stream for hiccl_reduce_plan_sync: for
+ * stream-ordered callers that synchronise the stream themselves, and for
+ * launches from several threads onto different streams. */
+int hiccl_reduce_plan_enqueue(hiccl_reduce_plan_t *plan, void *stream);
 /* Reference structure, for measurement: one kernel per compute, each on
  * the given stream (compute.h:88-91 launches one kernel per compute) --
  * each one a one-shot hiccl_reduce_ex with the plan's configuration (AUTO

@@ -581,3 +581,222 @@ def test_plain_c_client_on_gpu():
     assert os.path.exists(exe), "run make"
     p = subprocess.run(["timeout", "-k", "5", "60", exe, "gpu"], capture_output=True, text=True)
     assert p.returncode == 0 and "abi_c: PASSED" in p.stdout, p.stdout + p.stderr
+
+
+# ---------------------------------------------------------------------------
+# Config sizes exactly as BASELINE.json names them (sampled bitwise checks
+# against the oracle generator: a size-independent property at full size).
+
+def _sampled(out, n, count, seed, bf16=False, extra=()):
+    rng = np.random.default_rng(count % 1000003 + n)
+    idx = np.concatenate([np.arange(64), count - 64 + np.arange(64), rng.integers(0, count, 4096),
+                          np.asarray(extra, np.int64)]).astype(np.int64)
+    idx = idx[(idx >= 0) & (idx < count)]
+    got = out[torch.from_numpy(idx).to(DEV)]
+    got = got.view(torch.int16).cpu().numpy().view(np.uint16) if bf16 else got.cpu().numpy()
+    from conftest import Oracle
+    exp = Oracle().sample_sum(idx.astype(np.uint64), seed, n, bf16=bf16)
+    return bits_equal(got, exp), first_mismatch(got, exp)
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8, 16, 32, 64])
+def test_config3_exact_sizes(oracle, n):
+    """Config 3: n inputs x 2^26 fp32 (256 MiB each), the one-shot launch."""
+    count, seed = 1 << 26, 3000 + n
+    ins = [torch.empty(count, device=DEV) for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, seed, k)
+    out = torch.empty(count, device=DEV)
+    hiccl_amd.reduce(out, ins)
+    torch.cuda.synchronize()
+    ok, msg = _sampled(out, n, count, seed)
+    assert ok, msg
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_config4_exact_256MiB_in_1MiB_computes(oracle, dtype):
+    """Config 4: n = 8, 256 MiB per input split into 1 MiB computes with the
+    partition() formula (reduce.h:401-415), ONE batched plan launch."""
+    n, esz = 8, (2 if dtype == torch.bfloat16 else 4)
+    count, seed, depth = (256 << 20) // esz, 4000 + esz, 256
+    ins = [torch.empty(count, dtype=dtype, device=DEV) for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, seed, k)
+    out = torch.full((count,), float("nan"), dtype=dtype, device=DEV)
+    comp = hiccl_amd.Compute(dtype, device=0)
+    off = 0
+    for b in range(depth):
+        c = count // depth + (1 if b < count % depth else 0)
+        comp.add([(t, off) for t in ins], (out, off), c, compid=0)
+        off += c
+    assert off == count
+    comp.start(stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    # every compute's first and last element, plus the random sample
+    bounds = [b * (count // depth) + min(b, count % depth) for b in range(depth)]
+    ok, msg = _sampled(out, n, count, seed, bf16=(dtype == torch.bfloat16),
+                       extra=bounds + [x - 1 for x in bounds[1:]])
+    assert ok, msg
+    assert not torch.isnan(out.float()).any().item()  # no compute left unwritten
+    comp.close()
+
+
+def test_bf16_2pow31_elements_64bit_offsets(oracle):
+    """bf16 at 2^31 elements per input (4 GiB, n = 2): every byte offset past
+    2^32 -- checked around 2^31 elements and at the end, under both engines."""
+    n, count, seed = 2, 1 << 31, 77
+    free, _ = torch.cuda.mem_get_info()
+    if free < (n + 1) * count * 2 + (1 << 30):
+        pytest.skip("not enough device memory")
+    ins = [torch.empty(count, dtype=torch.bfloat16, device=DEV) for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, seed, k)
+    out = torch.empty(count, dtype=torch.bfloat16, device=DEV)
+    edge = [(1 << 30) - 1, 1 << 30, (1 << 31) - 8 + np.arange(8)]
+    extra = [int(x) for e in edge for x in np.atleast_1d(e)]
+    for eng in (None, PHASE, dict(engine=hiccl_amd.HICCL_ENGINE_TILE)):
+        out.view(torch.int16).fill_(-1)
+        hiccl_amd.reduce(out, ins, config=eng)
+        torch.cuda.synchronize()
+        ok, msg = _sampled(out, n, count, seed, bf16=True, extra=extra)
+        assert ok, (eng, msg)
+
+
+# ---------------------------------------------------------------------------
+# Plan configuration and capture rules
+
+@pytest.mark.parametrize("cfg", [
+    dict(engine=1, unroll=1, blocks_per_cu=4), dict(engine=1, unroll=2, blocks_per_cu=3),
+    dict(engine=1, unroll=4, schedule=2, grab=1), dict(engine=2), dict(engine=2, schedule=2),
+    dict(engine=1, grid=7), dict(blocks_per_cu=2)])
+@pytest.mark.parametrize("dtype", [np.float32, np.uint16], ids=["f32", "bf16"])
+def test_plan_config_same_bits(oracle, cfg, dtype):
+    """hiccl_reduce_plan_set_config: every honoured field gives the reference
+    bits on a ragged, misaligned batch."""
+    rng = np.random.default_rng(9)
+    tdt = TORCH_OF[np.dtype(dtype)]
+    comp = hiccl_amd.Compute(tdt, device=0, config=cfg)
+    outs, exps, keep = [], [], []
+    for c in range(9):
+        n = int(rng.integers(1, 10))
+        count = int(rng.integers(1, 300000))
+        x = oracle.fill(n, count, seed=70 + c, dtype=dtype)
+        ins = [to_dev(r).view(tdt) for r in x]
+        keep += ins
+        ob = torch.empty(count + 1, dtype=tdt, device=DEV)
+        comp.add(ins, (ob, 1), count, compid=0)
+        outs.append((ob, count))
+        exps.append(oracle.reduce(list(x), dtype=dtype))
+    for _ in range(2):
+        comp.start()
+        comp.wait()
+        for (ob, count), e in zip(outs, exps):
+            got = to_host(ob[1:1 + count], dtype)
+            assert bits_equal(got, e), (cfg, first_mismatch(got, e))
+    comp.close()
+
+
+def test_plan_config_refuses_unsupported_fields():
+    for bad in (dict(engine=1, unroll=8), dict(engine=2, unroll=4), dict(engine=1, block=512),
+                dict(nontemporal=1), dict(store_policy=3), dict(drain=1), dict(schedule=7)):
+        with pytest.raises(hiccl_amd.HicclError):
+            hiccl_amd.Compute(torch.float32, device=0, config=bad)
+    with pytest.raises(hiccl_amd.HicclError):  # unroll 2 exists for f32/bf16 only
+        hiccl_amd.Compute(torch.float64, device=0, config=dict(engine=1, unroll=2))
+
+
+def test_large_n_refuses_unsupported_shape():
+    """n > 64 runs on the plan kernel: a one-shot shape it lacks is an error,
+    not silently replaced (VERDICT r1 weak #9)."""
+    x = torch.zeros(1000, device=DEV)
+    with pytest.raises(hiccl_amd.HicclError, match="n > 64"):
+        hiccl_amd.reduce(x, [x] * 70, config=dict(block=512, unroll=4))
+    with pytest.raises(hiccl_amd.HicclError, match="n > 64"):
+        hiccl_amd.reduce(x, [x] * 70, config=dict(engine=2, nontemporal=1))
+
+
+@pytest.mark.parametrize("n", [65, 100])
+def test_large_n_capture_is_refused(n):
+    """A > 64-input one-shot call uploads its pointer table from host memory
+    per call: captured, the graph would replay a copy from a freed buffer --
+    the library refuses the capture with a clear error."""
+    count = 4099
+    ins = [torch.ones(count, device=DEV) for _ in range(n)]
+    out = torch.empty(count, device=DEV)
+    hiccl_amd.reduce(out, ins)  # eager: fine
+    torch.cuda.synchronize()
+    assert out[0].item() == float(n)
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(hiccl_amd.HicclError, match="cannot be captured"):
+        with torch.cuda.graph(g):
+            hiccl_amd.reduce(out, ins)
+
+
+def test_plan_capture_after_eager_upload(oracle):
+    """A plan's first launch after an add uploads its table (synchronous):
+    refused inside a capture; after one eager launch the plan captures and
+    every replay gives the reference bits."""
+    n, count = 6, 300001
+    x = oracle.fill(n, count, seed=41)
+    ins = [to_dev(r) for r in x]
+    out = torch.empty(count, device=DEV)
+    comp = hiccl_amd.Compute(torch.float32, device=0)
+    for b in range(3):
+        c = count // 3 + (1 if b < count % 3 else 0)
+        comp.add([(t, b * (count // 3) + min(b, count % 3)) for t in ins],
+                 (out, b * (count // 3) + min(b, count % 3)), c, compid=0)
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(hiccl_amd.HicclError, match="cannot be captured"):
+        with torch.cuda.graph(g, stream=s):
+            comp.start(stream=s)
+    comp.start(stream=s)  # eager: uploads
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        comp.start(stream=s)
+    for _ in range(3):
+        out.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        exp = oracle.reduce(list(x))
+        assert bits_equal(got, exp), first_mismatch(got, exp)
+    comp.close()
+
+
+def test_dynamic_schedule_per_thread_stream_two_threads(oracle):
+    """hipStreamPerThread is one handle value for a different stream on each
+    host thread: two threads launching dynamic-schedule reductions on it at
+    once must not share a ticket counter (the library takes the static
+    schedule there) -- both results bit-exact."""
+    import threading
+    n, count = 8, (1 << 22) + 5  # >= 32 tickets per workgroup: dynamic if allowed
+    xs = [oracle.fill(n, count, seed=s) for s in (1, 2)]
+    exps = [oracle.reduce(list(x)) for x in xs]
+    bufs = [([to_dev(r) for r in x], torch.empty(count, device=DEV)) for x in xs]
+    torch.cuda.synchronize()
+    PER_THREAD = 2  # hipStreamPerThread
+    errs = []
+
+    def work(i):
+        try:
+            torch.cuda.set_device(0)
+            ins, out = bufs[i]
+            for _ in range(20):
+                hiccl_amd.reduce(out, ins, stream=PER_THREAD,
+                                 config=dict(engine=hiccl_amd.HICCL_ENGINE_TILE,
+                                             schedule=hiccl_amd._lib.HICCL_SCHED_DYNAMIC))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for (ins, out), e in zip(bufs, exps):
+        got = out.cpu().numpy()
+        assert bits_equal(got, e), first_mismatch(got, e)

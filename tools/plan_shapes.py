@@ -117,6 +117,27 @@ def main():
             v += [(k, make(cfg)) for k, cfg in SWEEP]
         return v
 
+    if "launch" in shapes:
+        # launch overhead on the 16 MiB shape: plan launch (+ completion event),
+        # plan enqueue (no event), the one-shot launch, a 1-compute plan
+        count = 16 * MIB // 4
+        comp, ins, out = partitioned_plan(torch.float32, 8, count, 16)
+        one, _, _ = partitioned_plan(torch.float32, 8, count, 1)
+        runs = {"plan16_launch": lambda: comp.start(stream=stream), "plan16_enqueue": lambda: comp.enqueue(stream),
+                "plan1_enqueue": lambda: one.enqueue(stream), "oneshot": lambda: hiccl_amd.reduce(out, ins),
+                "plan16_launch_sync": lambda: (comp.start(stream=stream), comp.wait())}
+        res = {}
+        for _ in range(args.rounds):
+            for k, fn in runs.items():
+                ev, q = timeit(fn, args.steps, args.warmup)
+                res.setdefault(k, []).append((ev, q))
+        for k, v in res.items():
+            ev, q = float(np.median([x[0] for x in v])), float(np.median([x[1] for x in v]))
+            print(json.dumps({"shape": "launch_16MiB_f32", "variant": k, "event_us": round(ev * 1e3, 2),
+                              "queued_us": round(q * 1e3, 2), "queued_GBps": round(9 * count * 4 / q / 1e6, 1)}),
+                  flush=True)
+        comp.close()
+        one.close()
     if "a" in shapes:
         for dtype, dn in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
             esz = 2 if dtype == torch.bfloat16 else 4
