@@ -25,6 +25,11 @@ SHAPES = {  # grid threads -> (shape, algorithmic bytes per launch): tools/plan_
 }
 
 
+def kname(r):
+    n = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+    return n.split("(")[0]
+
+
 def grid_of(r):
     for k in ("Grid_Size", "Grid_Size_X"):
         if k in r and r[k]:
@@ -39,14 +44,14 @@ def main():
     rows = [r for r in csv.DictReader(open(trace)) if "k_reduce" in r["Kernel_Name"]]
     durs = {}
     for r in rows:
-        key = (r["Kernel_Name"].split("(")[0].replace("void (anonymous namespace)::", ""), grid_of(r))
+        key = (kname(r), grid_of(r))
         durs.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     counters = {}
     for f in sorted(glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
             if "k_reduce" not in r["Kernel_Name"]:
                 continue
-            key = (r["Kernel_Name"].split("(")[0].replace("void (anonymous namespace)::", ""), grid_of(r))
+            key = (kname(r), grid_of(r))
             counters.setdefault(key, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     out = []
     for key, ds in durs.items():
