@@ -958,8 +958,19 @@ int auto_bpc(int engine, uint64_t npkt, int dtype, int acc, int dev) {
              : kDefBpc;
 }
 
-// Fill in the engine and its default shape.
-void finish_cfg(Cfg &c, uint64_t npkt, int n, int dtype, int dev) {
+// Packets per lane of the TILE engine: a launch with fewer than two 16 KiB
+// tiles per CU is pure latency (one round trip per workgroup) -- half-size
+// tiles on twice the workgroups finish it sooner (the C5 step, four n = 2
+// and one n = 4 computes of 2^18 f32: 4.75 vs 5.32 us queued,
+// profiles/r02c_plan_sweep.jsonl); 2 exists for the headline types only.
+int auto_unroll(uint64_t npkt, int dtype, int acc, int dev) {
+  const bool tuned = dtype == HICCL_FLOAT32 || (dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_NATIVE);
+  return tuned && npkt < 2ull * device_cus(dev) * kDefBlock * kDefUnroll ? 2 : kDefUnroll;
+}
+
+// Fill in the engine and its default shape (n: inputs, or a plan's
+// packet-weighted mean).
+void finish_cfg(Cfg &c, uint64_t npkt, double n, int dtype, int dev) {
   if (c.engine == HICCL_ENGINE_AUTO)
     c.engine = (c.block || c.unroll) ? HICCL_ENGINE_TILE : auto_engine(npkt, n, dtype, c.acc, dev);
   if (c.engine == HICCL_ENGINE_PHASE) {
@@ -967,7 +978,7 @@ void finish_cfg(Cfg &c, uint64_t npkt, int n, int dtype, int dev) {
     if (!c.unroll) c.unroll = phase_p_dtype(dtype, c.acc);
   } else {
     if (!c.block) c.block = kDefBlock;
-    if (!c.unroll) c.unroll = kDefUnroll;
+    if (!c.unroll) c.unroll = auto_unroll(npkt, dtype, c.acc, dev);
   }
   if (!c.bpc) c.bpc = auto_bpc(c.engine, npkt, dtype, c.acc, dev);
 }
@@ -1072,6 +1083,7 @@ single_fn pick_single_dtype(int dtype, const Cfg &c) {
 // the headline types (f32, bf16 native).  Cache policy: nt loads and stores.
 
 constexpr int kPlanBlock = kDefBlock;
+static_assert(kPlanBlock == kDefBlock, "plan_cfg shapes plans with finish_cfg");
 
 // Packets per work unit (tile or chunk) of a plan kernel.
 uint64_t unit_pkts(int engine, int dtype, int acc, int unroll) {
@@ -1266,16 +1278,7 @@ namespace {
 // packets of packet-weighted mean `mean_n` inputs.
 Cfg plan_cfg(const hiccl_reduce_plan *p, uint64_t npkt, double mean_n) {
   Cfg c = resolve(&p->req);
-  if (c.engine == HICCL_ENGINE_AUTO)
-    c.engine = (c.block || c.unroll) ? HICCL_ENGINE_TILE : auto_engine(npkt, mean_n, p->dtype, c.acc, p->device);
-  if (c.engine == HICCL_ENGINE_PHASE) {
-    if (!c.block) c.block = kPhBlock;
-    if (!c.unroll) c.unroll = phase_p_dtype(p->dtype, c.acc);
-  } else {
-    if (!c.block) c.block = kPlanBlock;
-    if (!c.unroll) c.unroll = kDefUnroll;
-  }
-  if (!c.bpc) c.bpc = auto_bpc(c.engine, npkt, p->dtype, c.acc, p->device);
+  finish_cfg(c, npkt, mean_n, p->dtype, p->device);  // (kPlanBlock == kDefBlock)
   return c;
 }
 
