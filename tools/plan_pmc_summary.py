@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHAPES = {  # grid threads -> (shape, algorithmic bytes per launch): tools/plan_shapes.py
     262144: ("a: C4 16 MiB/input x 16 computes, n = 8 (f32 then bf16)", 9 * 16 << 20),
     65536: ("b: C4 bf16 1 GiB/input x 1024 computes, n = 8 (plan and one-shot)", 9 * 1024 << 20),
-    81920: ("c: C5 step, 4 x (n = 2) + 1 x (n = 4) computes of 2^18 f32", (4 * 3 + 5) * (1 << 18) * 4),
+    81920: ("c: C5 step, 4 x (n = 2) + 1 x (n = 4) computes of 2^18 f32 (U = 4)", (4 * 3 + 5) * (1 << 18) * 4),
+    163840: ("c: C5 step, 4 x (n = 2) + 1 x (n = 4) computes of 2^18 f32 (U = 2)", (4 * 3 + 5) * (1 << 18) * 4),
 }
 
 
