@@ -45,7 +45,9 @@ def run(exe, np_, args, env_extra=None, timeout=240):
 
 
 @pytest.mark.parametrize("np_,args", [(8, [1000, 1, 1, 4, 1, 2]), (8, [999, 2, 2, 3, 0, 1]),
-                                      (16, [257, 1, 1, 2, 0, 1])])
+                                      (16, [257, 1, 1, 2, 0, 1]),
+                                      # config 1: 2 ranks, 131072 elements = 1 MiB of size_t per chunk
+                                      (2, [131072, 1, 1, 1, 0, 1])])
 @pytest.mark.parametrize("pattern", range(1, 9))
 def test_reference_driver_host(pattern, np_, args):
     need(REF_HOST)
@@ -65,4 +67,17 @@ def test_reference_driver_gpu(pattern, streamed):
     need(REF_HIP)
     # keep the driver's own measure loops minimal
     rc, out = run(REF_HIP, 8, [pattern, 4099, 1, 1, 4, 0, 1], {"HICCL_STREAM_ORDERED": streamed})
+    assert f"VERIFY {NAMES[pattern]} ROOT = 0: PASSED!" in out, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", [4, 8])
+def test_config1_reference_driver_on_gpu_box_host(pattern):
+    """Config 1 (BASELINE.json configs[0]) on the GPU box's own host CPU: the
+    reference's unmodified collectives/main.cpp, host port (no GPU used), 2
+    MPI ranks, 1 MiB per rank per chunk, must print its KAT PASSED.  Marked
+    gpu so the round-end GPU tier records it on the box the CPU baseline is
+    timed on."""
+    need(REF_HOST)
+    rc, out = run(REF_HOST, 2, [pattern, 131072, 1, 1, 1, 0, 1])
     assert f"VERIFY {NAMES[pattern]} ROOT = 0: PASSED!" in out, out[-3000:]
