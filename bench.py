@@ -98,7 +98,17 @@ def init_control_plane():
     import torch.distributed as tdist
     if not tdist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        tdist.init_process_group("gloo")
+        # gloo announces its connections on stdout; the driver reads rank 0's
+        # stdout for the one JSON line, so route them to stderr
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            tdist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     return tdist
 
 
