@@ -485,9 +485,15 @@ def main():
     ap.add_argument("--c5-log2count", type=int, default=25,
                     help="config-5 leg: elements per rank per chunk = 2^x (25: 1 GiB fp32 send buffer at 8 ranks)")
     ap.add_argument("--c5-iters", type=int, default=5)
+    ap.add_argument("--c5", type=int, default=0, metavar="RANKS",
+                    help="run only the config-5 leg with RANKS MPI ranks (one per GPU when there are enough; "
+                         "otherwise a rehearsal with ranks sharing GPUs) and print its JSON")
     args = ap.parse_args()
     if args.cpu_leg:
         return cpu_leg(args)
+    if args.c5:
+        print(json.dumps({"mode": "c5", **run_c5(args.c5, args, allow_shared=True)}), flush=True)
+        return 0
 
     c5 = None
     if os.environ.get("WORLD_SIZE", "1") != "1" and not args.no_c5:
@@ -729,6 +735,21 @@ def schedsweep(args):
                     ("tile_dyn_b512u2", dict(engine=1, schedule=2, block=512, unroll=2)),
                     ("phase_static", dict(engine=2, schedule=1)),
                     ("phase_bpc2", dict(engine=2, schedule=1, blocks_per_cu=2))]
+    if args.sweepset == "widetile":  # few inputs: wide TILE tiles (32 packets per lane in flight)
+        variants = [("auto", None),
+                    ("phase_static", dict(engine=2, schedule=1)),
+                    ("tile_u4_static", dict(engine=1, schedule=1)),
+                    ("tile_u8_static", dict(engine=1, unroll=8, schedule=1)),
+                    ("tile_u8_dyn", dict(engine=1, unroll=8, schedule=2, grab=1)),
+                    ("tile_u16_static", dict(engine=1, unroll=16, schedule=1)),
+                    ("tile_u16_dyn", dict(engine=1, unroll=16, schedule=2, grab=1))]
+    if args.sweepset == "widedyn":  # wide tiles on the dynamic schedule vs AUTO, larger buckets
+        variants = [("auto", None),
+                    ("phase_static", dict(engine=2, schedule=1)),
+                    ("tile_u4_dyn", dict(engine=1, schedule=2)),
+                    ("tile_u8_dyn", dict(engine=1, unroll=8, schedule=2, grab=1)),
+                    ("tile_u8_dyn_g2", dict(engine=1, unroll=8, schedule=2, grab=2)),
+                    ("tile_u16_dyn", dict(engine=1, unroll=16, schedule=2, grab=1))]
     if args.sweepset == "xover":  # engine x schedule crossover (sets AUTO)
         variants = [("auto", None),
                     ("tile_dyn", dict(engine=1, schedule=2)),

@@ -375,16 +375,19 @@ __device__ __forceinline__ void tile_body(char *outb, Inputs in, uint32_t n, uin
   typename Op::acc_t acc[U];
 #pragma unroll
   for (int u = 0; u < U; u++) acc[u] = Op::zero();
+  // groups of GM inputs: at most 32 packets per lane in flight (U = 8: 4
+  // inputs, U = 16: 2), so wide tiles stay within the register file
+  constexpr uint32_t GM = U >= 8 ? 32 / U : 8;
   uint32_t g = 0;
-  for (; g + 8 <= n; g += 8) group_at<Op, U, 8, POL>(acc, in, g, tile_off, tile_bytes, voff);
+  for (; g + GM <= n; g += GM) group_at<Op, U, GM, POL>(acc, in, g, tile_off, tile_bytes, voff);
   switch (n - g) {  // wave-uniform
     case 1: group_at<Op, U, 1, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 2: group_at<Op, U, 2, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 3: group_at<Op, U, 3, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 4: group_at<Op, U, 4, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 5: group_at<Op, U, 5, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 6: group_at<Op, U, 6, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
-    case 7: group_at<Op, U, 7, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 2: if constexpr (GM > 2) group_at<Op, U, 2, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 3: if constexpr (GM > 3) group_at<Op, U, 3, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 4: if constexpr (GM > 4) group_at<Op, U, 4, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 5: if constexpr (GM > 5) group_at<Op, U, 5, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 6: if constexpr (GM > 6) group_at<Op, U, 6, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
+    case 7: if constexpr (GM > 7) group_at<Op, U, 7, POL>(acc, in, g, tile_off, tile_bytes, voff); break;
     default: break;
   }
   before_store();
@@ -757,22 +760,24 @@ constexpr double kTicketTiles = 9;
 // workgroup on: below it the phased engine is ahead.
 constexpr uint64_t kTileMinTicketsPerWG = 64;
 
-// Units per ticket of the dynamic schedule: one 128 KiB phased chunk; for
-// tiles enough to cover kTicketTiles tile-loads.
-uint32_t default_grab(int engine, double n) {
-  if (engine == HICCL_ENGINE_PHASE) return 1u;
+// Wide tiles (TILE, 256 lanes x 8 packets = 32 KiB per input) on the
+// dynamic schedule for few inputs (2..4) and large buckets: 32 packets per
+// lane in flight over the n inputs at once.  From 128 tickets per workgroup
+// (1 GiB per input) they lead the phased engine by 2-8 % (n = 2 / 3 / 4 at
+// 1-4 GiB per input: 6.34-6.47 / 6.26-6.60 / 6.17-6.51 vs 5.77-6.25 TB/s);
+// at 512 MiB they tie, at 256 MiB they lose (profiles/r02f_widetile_sweep.jsonl,
+// r02f_widedyn_sweep.jsonl).  f32 and bf16 (native accumulation) only.
+constexpr int kWideUnroll = 8;
+constexpr uint64_t kWideMinTicketsPerWG = 128;
+
+// Units per ticket of the dynamic schedule: one 128 KiB phased chunk or one
+// wide tile; for 16 KiB tiles enough to cover kTicketTiles tile-loads.
+uint32_t default_grab(int engine, double n, int unroll = 4 /* kDefUnroll */) {
+  if (engine == HICCL_ENGINE_PHASE || unroll >= kWideUnroll) return 1u;
   const double g = kTicketTiles / (n + 1.0);
   return g <= 1.0 ? 1u : (uint32_t)(g + 0.999);
 }
 
-// The counter pair for a launch of `units` work units (n inputs, packet-
-// weighted mean for a plan) on `grid` workgroups on (dev, s), or NULL for a
-// static schedule: AUTO is dynamic for the TILE engine from kDynMinInputs
-// inputs (with the static grid-stride each workgroup is bound to the same
-// addresses mod grid x 16 KiB, i.e. to a fixed subset of DRAM channels, and
-// the ones on slow channels straggle: 5.6-5.7 vs 6.3-6.7 TB/s on C2); never
-// during stream capture (a replayed graph could run beside other work on
-// the same stream's counter); NULL also on any allocation failure.
 // Is `s` being captured into a graph?  `if_unknown` is the answer when the
 // runtime cannot tell.
 bool capturing(hipStream_t s, bool if_unknown) {
@@ -791,11 +796,22 @@ bool capturing(hipStream_t s, bool if_unknown) {
 // streams): launches on it serialise, one counter is safe.
 bool per_thread_stream(hipStream_t s) { return s == hipStreamPerThread; }
 
+// The counter pair for a launch of `units` work units (n inputs, packet-
+// weighted mean for a plan) on `grid` workgroups on (dev, s), or NULL for a
+// static schedule: AUTO is dynamic for the TILE engine from kDynMinInputs
+// inputs or with wide tiles (with the static grid-stride each workgroup is
+// bound to the same addresses mod grid x 16 KiB, i.e. to a fixed subset of
+// DRAM channels, and the ones on slow channels straggle: 5.6-5.7 vs
+// 6.3-6.7 TB/s on C2); never during stream capture (a replayed graph could
+// run beside other work on the same stream's counter) nor on
+// hipStreamPerThread; NULL also on any allocation failure.
 uint32_t *unit_sched_for(int engine, double n, uint64_t units, uint64_t grid, int dev, hipStream_t s,
-                         int schedule = HICCL_SCHED_AUTO, uint32_t grab = 0) {
+                         int schedule = HICCL_SCHED_AUTO, uint32_t grab = 0, int unroll = 4 /* kDefUnroll */) {
   if (schedule == HICCL_SCHED_STATIC) return nullptr;
-  if (schedule == HICCL_SCHED_AUTO && (engine != HICCL_ENGINE_TILE || n < kDynMinInputs)) return nullptr;
-  if (!grab) grab = default_grab(engine, n);
+  if (schedule == HICCL_SCHED_AUTO &&
+      (engine != HICCL_ENGINE_TILE || (n < kDynMinInputs && unroll < kWideUnroll)))
+    return nullptr;
+  if (!grab) grab = default_grab(engine, n, unroll);
   if ((units + grab - 1) / grab < kDynMinUnitsPerWG * grid) return nullptr;
   if (per_thread_stream(s) || capturing(s, true)) return nullptr;
   std::lock_guard<std::mutex> lk(g_sched_mu);
@@ -878,6 +894,7 @@ int check_buffers(void *out, const void *const *in, int n, size_t count, size_t 
 // Both: nt loads and nt stores, one workgroup per CU, grid-stride.
 constexpr int kDefBlock = 256;
 constexpr int kDefUnroll = 4;
+static_assert(kDefUnroll == 4, "default_grab / unit_sched_for default their unroll to 4");
 constexpr int kDefPol = 11;  // nt loads, nt stores
 constexpr int kDefBpc = 1;
 constexpr int kSmallBpc = 4;
@@ -932,7 +949,16 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
 // (n = 8, 1 GiB: 6.71 vs 6.32 TB/s phased), the phased engine below it
 // (n = 8, 128 MiB = 32 tickets: 6.41 vs 5.94); with <= 4 inputs the phased
 // engine leads at every size with a chunk per CU (r01_schedsweep.jsonl).
+// Wide tiles (kWideUnroll) for this launch?  (f32 / bf16 native, 2..4 inputs,
+// >= kWideMinTicketsPerWG wide tiles per workgroup.)
+bool auto_wide(uint64_t npkt, double n, int dtype, int acc, int dev) {
+  const bool tuned = dtype == HICCL_FLOAT32 || (dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_NATIVE);
+  return tuned && n >= 1.5 && n < kDynMinInputs &&
+         npkt / ((uint64_t)kDefBlock * kWideUnroll) >= kWideMinTicketsPerWG * (uint64_t)device_cus(dev);
+}
+
 int auto_engine(uint64_t npkt, double n, int dtype, int acc, int dev) {
+  if (auto_wide(npkt, n, dtype, acc, dev)) return HICCL_ENGINE_TILE;
   const bool packed_ok = !(dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_WIDE);
   if (n >= kDynMinInputs && packed_ok) {
     const uint64_t tickets = npkt / ((uint64_t)kDefBlock * kDefUnroll) / default_grab(HICCL_ENGINE_TILE, n);
@@ -978,7 +1004,7 @@ void finish_cfg(Cfg &c, uint64_t npkt, double n, int dtype, int dev) {
     if (!c.unroll) c.unroll = phase_p_dtype(dtype, c.acc);
   } else {
     if (!c.block) c.block = kDefBlock;
-    if (!c.unroll) c.unroll = auto_unroll(npkt, dtype, c.acc, dev);
+    if (!c.unroll) c.unroll = auto_wide(npkt, n, dtype, c.acc, dev) ? kWideUnroll : auto_unroll(npkt, dtype, c.acc, dev);
   }
   if (!c.bpc) c.bpc = auto_bpc(c.engine, npkt, dtype, c.acc, dev);
 }
@@ -1011,6 +1037,9 @@ single_fn pick_u(int u, int pol) {
     case 1: return pick_nt<Op, B, 1>(pol);
     case 2: return pick_nt<Op, B, 2>(pol);
     case 4: return pick_nt<Op, B, 4>(pol);
+    // wide tiles for few inputs (32 packets per lane in flight at n = 4 / 2)
+    case 8: return pol == kDefPol && B == 256 ? launch_single_t<Op, B, 8, kDefPol> : nullptr;
+    case 16: return pol == kDefPol && B == 256 ? launch_single_t<Op, B, 16, kDefPol> : nullptr;
     default: return nullptr;
   }
 }
@@ -1106,6 +1135,8 @@ plan_fn pick_plan_eng(int engine, int unroll) {
     case 0:
     case 4: return launch_plan_t<Op, kTile, 4>;
     case 2: if constexpr (TUNED) return launch_plan_t<Op, kTile, 2>; break;
+    case 8: if constexpr (TUNED) return launch_plan_t<Op, kTile, 8>; break;
+    case 16: if constexpr (TUNED) return launch_plan_t<Op, kTile, 16>; break;
     case 1: if constexpr (TUNED) return launch_plan_t<Op, kTile, 1>; break;
     default: break;
   }
@@ -1140,7 +1171,7 @@ std::string plan_shape_error(const Cfg &c, int dtype) {
   }
   if (c.block != kPlanBlock) return "plan kernels run the TILE engine at block 256 only";
   if (!pick_plan(dtype, c.acc, HICCL_ENGINE_TILE, c.unroll))
-    return "plan kernels run the TILE engine at unroll 4 (f32 / bf16: 1, 2 or 4) only";
+    return "plan kernels run the TILE engine at unroll 4 (f32 / bf16: 1, 2, 4, 8 or 16) only";
   return "";
 }
 
@@ -1223,9 +1254,9 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
 
   uint64_t grid = c.grid > 0 ? (uint64_t)c.grid : (uint64_t)device_cus(dev) * c.bpc;
   if (grid > a.ntiles) grid = a.ntiles;
-  a.grab = c.grab > 0 ? (uint32_t)c.grab : default_grab(c.engine, n);
+  a.grab = c.grab > 0 ? (uint32_t)c.grab : default_grab(c.engine, n, c.unroll);
   a.drain = (uint32_t)c.drain;
-  a.sched = unit_sched_for(c.engine, n, a.ntiles, grid, dev, s, c.schedule, a.grab);
+  a.sched = unit_sched_for(c.engine, n, a.ntiles, grid, dev, s, c.schedule, a.grab, c.unroll);
   fn(a, dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "hiccl_reduce: launch");
 }
@@ -1372,8 +1403,8 @@ int launch_plan(PlanArgs a, int dtype, const Cfg &c, double mean_n, int dev, hip
   const uint64_t units = a.t_end - a.t_begin;
   uint64_t grid = c.grid > 0 ? (uint64_t)c.grid : (uint64_t)device_cus(dev) * c.bpc;
   if (grid > units) grid = units;
-  a.grab = c.grab > 0 ? (uint32_t)c.grab : default_grab(c.engine, mean_n);
-  a.sched = unit_sched_for(c.engine, mean_n, units, grid, dev, s, c.schedule, a.grab);
+  a.grab = c.grab > 0 ? (uint32_t)c.grab : default_grab(c.engine, mean_n, c.unroll);
+  a.sched = unit_sched_for(c.engine, mean_n, units, grid, dev, s, c.schedule, a.grab, c.unroll);
   fn(a, dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "plan: launch");
 }

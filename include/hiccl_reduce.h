@@ -122,7 +122,8 @@ int hiccl_reduce_bf16(uint16_t *out, const uint16_t *const *in, int n, size_t co
  * be captured into a graph (hipErrorStreamCaptureUnsupported). */
 typedef struct {
   int block;         /* threads per workgroup: TILE 256 or 512; PHASE 256, 512 or 1024 */
-  int unroll;        /* 16-byte packets per input per lane per tile: TILE 1, 2 or 4;
+  int unroll;        /* 16-byte packets per input per lane per tile: TILE 1, 2 or 4 (block
+                        256, f32 / bf16: also 8 or 16 -- wide tiles for few inputs);
                         PHASE 4, 8 or 16 (chunk = block * unroll * 16 B) */
   int blocks_per_cu; /* persistent grid = CUs x this (capped by tiles) */
   int nontemporal;   /* loads: 1 plain cache policy, 2 nt */
@@ -176,7 +177,7 @@ int hiccl_reduce_plan_set_engine(hiccl_reduce_plan_t *plan, int engine);
 /* Kernel configuration of the plan's launches (NULL = all defaults; replaces
  * earlier set_engine / set_acc choices).  Honoured: engine, schedule, grab,
  * blocks_per_cu, grid, acc, and the TILE shape block 256 x unroll 4 (f32 and
- * bf16 also unroll 1 or 2); PHASE runs its default shape; loads and stores
+ * bf16 also unroll 1, 2, 8 or 16); PHASE runs its default shape; loads and stores
  * are nt.  Anything else is refused with hipErrorInvalidValue -- no field is
  * silently ignored. */
 int hiccl_reduce_plan_set_config(hiccl_reduce_plan_t *plan, const hiccl_reduce_config_t *cfg);

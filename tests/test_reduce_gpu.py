@@ -266,7 +266,8 @@ def test_phase_unsupported_shape_is_an_error():
     dict(block=256, unroll=2, nontemporal=1), dict(block=256, unroll=2, nontemporal=2, store_policy=2),
     dict(block=256, unroll=4, nontemporal=1, store_policy=3, grid=192),
     dict(block=512, unroll=4, nontemporal=2, store_policy=2, blocks_per_cu=2),
-    dict(block=256, unroll=1, grid=7)])
+    dict(block=256, unroll=1, grid=7), dict(block=256, unroll=8), dict(block=256, unroll=16),
+    dict(block=256, unroll=8, schedule=2, grab=1, grid=3), dict(block=256, unroll=16, grid=5)])
 def test_tuning_variants_same_bits(oracle, config):
     for n, count in ((8, 1 << 20), (3, 123457)):
         x = oracle.fill(n, count, seed=n)
@@ -407,6 +408,43 @@ def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
             ref = (ref + exp).astype(np.float32)
         assert bits_equal(got, ref)
         comp.close()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_auto_wide_tiles_large_few_inputs(oracle, dtype, n):
+    """AUTO at 1 GiB per input with 2-4 inputs: TILE with 32 KiB-per-input
+    tiles on the dynamic schedule (plan and one-shot), bit-exact vs the
+    in-order sum (sampled) and vs the forced phased engine."""
+    esz = 2 if dtype == torch.bfloat16 else 4
+    count = (1 << 30) // esz
+    base = torch.empty(count + 8, dtype=dtype, device=DEV)
+    hiccl_amd.fill_uniform(base, 55 + n, 0)
+    ins = [(base, k) for k in range(n)]  # mutually misaligned views of one buffer
+    outs = {}
+    for name, eng in (("auto", hiccl_amd.HICCL_ENGINE_AUTO), ("phase", hiccl_amd.HICCL_ENGINE_PHASE)):
+        out = torch.empty(count, dtype=dtype, device=DEV)
+        comp = hiccl_amd.Compute(dtype, device=0, engine=eng)
+        comp.add(ins, out, count, compid=0)
+        comp.start()
+        comp.wait()
+        if name == "auto" and torch.cuda.get_device_properties(0).multi_processor_count == 256:
+            assert comp.engine() == hiccl_amd.HICCL_ENGINE_TILE
+        comp.close()
+        outs[name] = out
+    one = torch.empty(count, dtype=dtype, device=DEV)
+    hiccl_amd.reduce(one, [base[k:k + count] for k in range(n)])
+    torch.cuda.synchronize()
+    iv = lambda t: t.view(torch.int16 if dtype == torch.bfloat16 else torch.int32)  # noqa: E731
+    assert torch.equal(iv(outs["auto"]), iv(outs["phase"]))
+    assert torch.equal(iv(outs["auto"]), iv(one))
+    idx = torch.randint(0, count, (4096,), generator=torch.Generator().manual_seed(n))
+    idx[:2] = torch.tensor([0, count - 1])
+    host = base.cpu()
+    acc = torch.zeros(idx.numel(), dtype=dtype)
+    for k in range(n):  # T acc = 0; acc += in[k][i] (compute.h:7-9)
+        acc = (acc.float() + host[idx + k].float()).to(dtype)
+    assert torch.equal(iv(outs["auto"][idx.to(DEV)].cpu()), iv(acc))
 
 
 def test_plan_auto_engine_bf16():
