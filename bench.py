@@ -746,7 +746,7 @@ def schedsweep(args):
     if args.sweepset == "widedyn":  # wide tiles on the dynamic schedule vs AUTO, larger buckets
         variants = [("auto", None),
                     ("phase_static", dict(engine=2, schedule=1)),
-                    ("tile_u4_dyn", dict(engine=1, schedule=2)),
+                    ("tile_u4_dyn", dict(engine=1, unroll=4, schedule=2)),
                     ("tile_u8_dyn", dict(engine=1, unroll=8, schedule=2, grab=1)),
                     ("tile_u8_dyn_g2", dict(engine=1, unroll=8, schedule=2, grab=2)),
                     ("tile_u16_dyn", dict(engine=1, unroll=16, schedule=2, grab=1))]

@@ -941,6 +941,17 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
   return r;
 }
 
+// Wide tiles for this launch: the unroll (16 for two inputs, 8 for three or
+// four: n = 2 at 1-2 GiB per input 6.50-6.66 vs 6.33-6.46 TB/s at 8; n = 3 / 4
+// lead at 8, profiles/r02g_wideverify.jsonl), or 0.  f32 / bf16 native only,
+// from kWideMinTicketsPerWG 8-packet tiles per workgroup (1 GiB per input).
+int auto_wide_unroll(uint64_t npkt, double n, int dtype, int acc, int dev) {
+  const bool tuned = dtype == HICCL_FLOAT32 || (dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_NATIVE);
+  if (!tuned || n < 1.5 || n >= kDynMinInputs) return 0;
+  if (npkt / ((uint64_t)kDefBlock * kWideUnroll) < kWideMinTicketsPerWG * (uint64_t)device_cus(dev)) return 0;
+  return n < 2.5 ? 2 * kWideUnroll : kWideUnroll;
+}
+
 // Auto engine from the packets per input of a launch (summed over its
 // computes) and the number of inputs (packet-weighted mean for a plan).
 // Interleaved engine x schedule sweeps, n = 5 / 8 / 16 x 32 MiB-1 GiB per
@@ -948,17 +959,10 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
 // tile engine on the dynamic schedule leads from 64 tickets per workgroup
 // (n = 8, 1 GiB: 6.71 vs 6.32 TB/s phased), the phased engine below it
 // (n = 8, 128 MiB = 32 tickets: 6.41 vs 5.94); with <= 4 inputs the phased
-// engine leads at every size with a chunk per CU (r01_schedsweep.jsonl).
-// Wide tiles (kWideUnroll) for this launch?  (f32 / bf16 native, 2..4 inputs,
-// >= kWideMinTicketsPerWG wide tiles per workgroup.)
-bool auto_wide(uint64_t npkt, double n, int dtype, int acc, int dev) {
-  const bool tuned = dtype == HICCL_FLOAT32 || (dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_NATIVE);
-  return tuned && n >= 1.5 && n < kDynMinInputs &&
-         npkt / ((uint64_t)kDefBlock * kWideUnroll) >= kWideMinTicketsPerWG * (uint64_t)device_cus(dev);
-}
-
+// engine leads at every size with a chunk per CU (r01_schedsweep.jsonl) --
+// except from 1 GiB per input, where wide tiles lead (auto_wide_unroll).
 int auto_engine(uint64_t npkt, double n, int dtype, int acc, int dev) {
-  if (auto_wide(npkt, n, dtype, acc, dev)) return HICCL_ENGINE_TILE;
+  if (auto_wide_unroll(npkt, n, dtype, acc, dev)) return HICCL_ENGINE_TILE;
   const bool packed_ok = !(dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_WIDE);
   if (n >= kDynMinInputs && packed_ok) {
     const uint64_t tickets = npkt / ((uint64_t)kDefBlock * kDefUnroll) / default_grab(HICCL_ENGINE_TILE, n);
@@ -1004,7 +1008,10 @@ void finish_cfg(Cfg &c, uint64_t npkt, double n, int dtype, int dev) {
     if (!c.unroll) c.unroll = phase_p_dtype(dtype, c.acc);
   } else {
     if (!c.block) c.block = kDefBlock;
-    if (!c.unroll) c.unroll = auto_wide(npkt, n, dtype, c.acc, dev) ? kWideUnroll : auto_unroll(npkt, dtype, c.acc, dev);
+    if (!c.unroll) {
+      const int wide = auto_wide_unroll(npkt, n, dtype, c.acc, dev);
+      c.unroll = wide ? wide : auto_unroll(npkt, dtype, c.acc, dev);
+    }
   }
   if (!c.bpc) c.bpc = auto_bpc(c.engine, npkt, dtype, c.acc, dev);
 }

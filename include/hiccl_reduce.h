@@ -56,10 +56,13 @@ typedef enum {
  *          added), then writes the chunk.
  *   AUTO   TILE (on the dynamic schedule, below) with >= 5 inputs once
  *          every workgroup gets >= 64 tickets (bf16: packed accumulator
- *          only); otherwise PHASE when every CU gets >= 1 chunk (two
- *          inputs: not at 2-16 chunks per CU, where TILE leads), else TILE
- *          with 4 workgroups per CU (one-shot: that call; plan: all
- *          computes, packet-weighted mean n). */
+ *          only); TILE with 32 KiB-per-input tiles (unroll 8) on the
+ *          dynamic schedule with 2-4 inputs once every workgroup gets
+ *          >= 128 of them (1 GiB per input, f32 / bf16); otherwise PHASE
+ *          when every CU gets >= 1 chunk (two inputs: not at 2-16 chunks
+ *          per CU, where TILE leads), else TILE with 4 workgroups per CU
+ *          (unroll 2 below two 16 KiB tiles per CU) (one-shot: that call;
+ *          plan: all computes, packet-weighted mean n). */
 typedef enum {
   HICCL_ENGINE_AUTO = 0,
   HICCL_ENGINE_TILE = 1,

@@ -735,7 +735,7 @@ def test_plan_config_same_bits(oracle, cfg, dtype):
 
 
 def test_plan_config_refuses_unsupported_fields():
-    for bad in (dict(engine=1, unroll=8), dict(engine=2, unroll=4), dict(engine=1, block=512),
+    for bad in (dict(engine=1, unroll=32), dict(engine=1, unroll=3), dict(engine=2, unroll=4), dict(engine=1, block=512),
                 dict(nontemporal=1), dict(store_policy=3), dict(drain=1), dict(schedule=7)):
         with pytest.raises(hiccl_amd.HicclError):
             hiccl_amd.Compute(torch.float32, device=0, config=bad)
