@@ -162,6 +162,12 @@ def run_c5(world, args, allow_shared=False):
         os.close(fd)
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_DRIVER_JSON=path, OMP_NUM_THREADS="1",
                    HICCL_SIGNAL_TIMEOUT="20", **extra)
+        if ndev < world:
+            # a rehearsal with ranks sharing GPUs: HIP's 4 hardware queues per
+            # process oversubscribe a device at 8 ranks and the queues
+            # time-slice (2.6 s instead of ~0.08 s per run,
+            # profiles/r02i_c5_rehearsal_1gpu.jsonl)
+            env["GPU_MAX_HW_QUEUES"] = "2"
         cmd = ["timeout", "-k", "10", "150", mpirun, "-np", str(world), C5_EXE, "8", str(count), "1", "1", "128",
                "2", str(args.c5_iters), hier, libs]
         t0 = time.perf_counter()
