@@ -156,6 +156,7 @@ def run_c5(world, args, allow_shared=False):
     out = {"workload": f"C5: all-reduce of {count * world * 4 >> 20} MiB fp32 per rank, {world} ranks, hierarchy "
                        f"{{{hier}}} {{{libs}}}, pipedepth 128 (collectives/main.cpp:151-155)"}
     modes = (("host", {"HICCL_STREAM_ORDERED": "0"}),
+             ("stream_graph", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "0"}),
              ("stream_graph_fused", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "1"}))
     for name, extra in modes:
         fd, path = tempfile.mkstemp(prefix="hiccl_c5_", suffix=".json", dir="/tmp")

@@ -19,7 +19,7 @@ def test_c5_leg_rehearsal_two_ranks_one_gpu():
     import bench
     res = bench.run_c5(2, argparse.Namespace(c5_log2count=16, c5_iters=2), allow_shared=True)
     assert "workload" in res, res
-    for mode in ("host", "stream_graph_fused"):
+    for mode in ("host", "stream_graph", "stream_graph_fused"):
         r = res[mode]
         assert r.get("kat") == "PASSED", r
         assert r["ranks"] == 2 and r["pipedepth"] == 128
