@@ -158,7 +158,12 @@ def run_c5(world, args, allow_shared=False):
     modes = (("host", {"HICCL_STREAM_ORDERED": "0"}),
              ("stream_graph", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "0"}),
              ("stream_graph_fused", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "1"}))
+    deadline = time.perf_counter() + 300.0  # the whole leg: never more than ~5 min of the bench run
     for name, extra in modes:
+        left = int(deadline - time.perf_counter())
+        if left < 30:
+            out[name] = {"skipped": "time budget of the config-5 leg spent"}
+            continue
         fd, path = tempfile.mkstemp(prefix="hiccl_c5_", suffix=".json", dir="/tmp")
         os.close(fd)
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_DRIVER_JSON=path, OMP_NUM_THREADS="1",
@@ -169,7 +174,7 @@ def run_c5(world, args, allow_shared=False):
             # time-slice (2.6 s instead of ~0.08 s per run,
             # profiles/r02i_c5_rehearsal_1gpu.jsonl)
             env["GPU_MAX_HW_QUEUES"] = "2"
-        cmd = ["timeout", "-k", "10", "150", mpirun, "-np", str(world), C5_EXE, "8", str(count), "1", "1", "128",
+        cmd = ["timeout", "-k", "10", str(min(120, left)), mpirun, "-np", str(world), C5_EXE, "8", str(count), "1", "1", "128",
                "2", str(args.c5_iters), hier, libs]
         t0 = time.perf_counter()
         p = subprocess.run(cmd, env=env, capture_output=True, text=True, cwd="/tmp")
