@@ -171,7 +171,7 @@ def run_c5(world, args, allow_shared=False):
         if ndev < world:
             # a rehearsal with ranks sharing GPUs: HIP's 4 hardware queues per
             # process oversubscribe a device at 8 ranks and the queues
-            # time-slice (2.6 s instead of ~0.08 s per run,
+            # time-slice (2.6 s instead of 24 ms per run at 8 ranks,
             # profiles/r02i_c5_rehearsal_1gpu.jsonl)
             env["GPU_MAX_HW_QUEUES"] = "2"
         cmd = ["timeout", "-k", "10", str(min(120, left)), mpirun, "-np", str(world), C5_EXE, "8", str(count), "1", "1", "128",

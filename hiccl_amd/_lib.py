@@ -101,6 +101,7 @@ _SIGS = {
     "hiccl_signal_wait_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_uint32, _vp, _vp,
                                              ctypes.c_double, _vp]),
     "hiccl_counter_add": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp]),
+    "hiccl_signal_wait_phases": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, ctypes.c_double, _vp]),
 }
 
 

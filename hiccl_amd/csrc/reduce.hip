@@ -679,33 +679,54 @@ __global__ void k_copy_bytes(char *dst, const char *src, uint64_t nbytes) {
 // bounded (s_memrealtime, 100 MHz): on timeout the lane records an error and
 // exits, so a broken protocol can never hang the GPU.
 
-constexpr int kMaxFlags = 64;
+constexpr int kMaxFlags = 64;  // signal and wait flags per launch (one per lane)
 
-struct SigWaitArgs {
+// Several signal/wait phases in ONE launch, executed in order: phase p
+// stores its epoch to its flags (system-scope release), then waits for its
+// flags (system-scope acquire); phase p + 1 starts after every wait of phase
+// p has finished.  The transport queues the consecutive signal/wait steps of
+// a stream-ordered pipeline (a step's done tokens, the next step's readies)
+// into one such launch instead of one launch each: same order of every
+// operation on the stream, fewer kernel boundaries (~1.5-1.9 us each).
+constexpr int kMaxPhases = 8;
+
+struct SigPhaseArgs {
   uint32_t *sig[kMaxFlags];
   const uint32_t *wait[kMaxFlags];
   uint32_t *err;
-  const uint32_t *epoch_dev;  // NULL, or a device word added to epoch at run time (graph replays)
+  const uint32_t *epoch_dev;  // NULL, or a device word added to every epoch at run time (graph replays)
   uint64_t timeout_ticks;
-  uint32_t nsig, nwait, epoch, pad;
+  uint32_t nphase, pad;
+  uint32_t sig_end[kMaxPhases];   // phase p signals sig[sig_end[p-1] .. sig_end[p])
+  uint32_t wait_end[kMaxPhases];  // and waits for wait[wait_end[p-1] .. wait_end[p])
+  uint32_t epoch[kMaxPhases];
 };
 
-__global__ __launch_bounds__(64) void k_sigwait(SigWaitArgs a) {
+__global__ __launch_bounds__(64) void k_sigwait_phases(SigPhaseArgs a) {
   const uint32_t lane = threadIdx.x;
-  uint32_t epoch = a.epoch;
-  if (a.epoch_dev) epoch += __hip_atomic_load(a.epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (lane < a.nsig) __hip_atomic_store(a.sig[lane], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (lane < a.nwait) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int32_t)(__hip_atomic_load(a.wait[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      __builtin_amdgcn_s_sleep(2);
-      // an earlier timeout (any wait of this rank) ends every later spin at once
-      if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-        if (a.err) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
+  const uint32_t add = a.epoch_dev ? __hip_atomic_load(a.epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  uint32_t s0 = 0, w0 = 0;
+  for (uint32_t p = 0; p < a.nphase; p++) {
+    const uint32_t epoch = a.epoch[p] + add;
+    const uint32_t s1 = a.sig_end[p], w1 = a.wait_end[p];
+    if (s0 + lane < s1) __hip_atomic_store(a.sig[s0 + lane], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (w0 + lane < w1) {
+      const uint32_t *f = a.wait[w0 + lane];
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((int32_t)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+          if (a.err) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
       }
     }
+    // every lane's waits of this phase precede any store of the next one
+    __syncthreads();
+    __atomic_thread_fence(__ATOMIC_ACQ_REL);
+    s0 = s1;
+    w0 = w1;
   }
 }
 
@@ -1751,30 +1772,76 @@ int hiccl_counter_add(uint32_t *ctr, uint32_t v, void *stream) {
 int hiccl_signal_wait_dev(uint32_t *const *sig, int nsig, const uint32_t *const *wait, int nwait,
                           uint32_t epoch, const uint32_t *epoch_dev, uint32_t *err, double timeout_s,
                           void *stream) {
-  if (nsig < 0 || nwait < 0 || (nsig && !sig) || (nwait && !wait))
-    return fail(hipErrorInvalidValue, "signal_wait: bad flag lists");
+  hiccl_signal_phase_t ph;
+  ph.sig = sig;
+  ph.nsig = nsig;
+  ph.wait = wait;
+  ph.nwait = nwait;
+  ph.epoch = epoch;
+  return hiccl_signal_wait_phases(&ph, 1, epoch_dev, err, timeout_s, stream);
+}
+
+int hiccl_signal_wait_phases(const hiccl_signal_phase_t *ph, int nph, const uint32_t *epoch_dev, uint32_t *err,
+                             double timeout_s, void *stream) {
+  if (nph < 0 || (nph && !ph)) return fail(hipErrorInvalidValue, "signal_wait: bad phase list");
+  for (int p = 0; p < nph; p++) {
+    const hiccl_signal_phase_t &q = ph[p];
+    if (q.nsig < 0 || q.nwait < 0 || (q.nsig && !q.sig) || (q.nwait && !q.wait))
+      return fail(hipErrorInvalidValue, "signal_wait: bad flag lists");
+    for (int i = 0; i < q.nsig; i++)
+      if (!q.sig[i]) return fail(hipErrorInvalidValue, "signal_wait: NULL signal flag");
+    for (int i = 0; i < q.nwait; i++)
+      if (!q.wait[i]) return fail(hipErrorInvalidValue, "signal_wait: NULL wait flag");
+  }
   const uint64_t ticks = (uint64_t)((timeout_s > 0 ? timeout_s : 30.0) * 1e8);  // s_memrealtime: 100 MHz
   hipStream_t s = (hipStream_t)stream;
-  int i = 0, j = 0;
-  while (i < nsig || j < nwait) {  // kMaxFlags of each per launch, in order
-    SigWaitArgs a;
+  SigPhaseArgs a;
+  auto reset = [&]() {
     memset(&a, 0, sizeof(a));
     a.err = err;
     a.epoch_dev = epoch_dev;
     a.timeout_ticks = ticks;
-    a.epoch = epoch;
-    for (; i < nsig && a.nsig < (uint32_t)kMaxFlags; i++) {
-      if (!sig[i]) return fail(hipErrorInvalidValue, "signal_wait: NULL signal flag");
-      a.sig[a.nsig++] = sig[i];
+  };
+  auto launch = [&]() -> int {
+    if (!a.nphase) return 0;
+    hipLaunchKernelGGL(k_sigwait_phases, dim3(1), dim3(64), 0, s, a);
+    int e = check_hip(hipGetLastError(), "signal_wait: launch");
+    reset();
+    return e;
+  };
+  // Append (sig[0..ns), wait[0..nw)) with `epoch` as one sub-phase, starting
+  // a new launch when the kernel's arrays or phase slots are full.
+  auto push = [&](uint32_t *const *sg, int ns, const uint32_t *const *wt, int nw, uint32_t epoch) -> int {
+    if (a.nphase == (uint32_t)kMaxPhases ||
+        (a.nphase ? a.sig_end[a.nphase - 1] : 0) + ns > (uint32_t)kMaxFlags ||
+        (a.nphase ? a.wait_end[a.nphase - 1] : 0) + nw > (uint32_t)kMaxFlags)
+      if (int e = launch()) return e;
+    const uint32_t s0 = a.nphase ? a.sig_end[a.nphase - 1] : 0, w0 = a.nphase ? a.wait_end[a.nphase - 1] : 0;
+    for (int i = 0; i < ns; i++) a.sig[s0 + i] = sg[i];
+    for (int i = 0; i < nw; i++) a.wait[w0 + i] = wt[i];
+    a.sig_end[a.nphase] = s0 + ns;
+    a.wait_end[a.nphase] = w0 + nw;
+    a.epoch[a.nphase] = epoch;
+    a.nphase++;
+    return 0;
+  };
+  reset();
+  for (int p = 0; p < nph; p++) {
+    const hiccl_signal_phase_t &q = ph[p];
+    if (q.nsig + q.nwait == 0) continue;
+    if (q.nsig <= kMaxFlags && q.nwait <= kMaxFlags) {
+      if (int e = push(q.sig, q.nsig, q.wait, q.nwait, q.epoch)) return e;
+      continue;
     }
-    for (; j < nwait && a.nwait < (uint32_t)kMaxFlags; j++) {
-      if (!wait[j]) return fail(hipErrorInvalidValue, "signal_wait: NULL wait flag");
-      a.wait[a.nwait++] = wait[j];
-    }
-    hipLaunchKernelGGL(k_sigwait, dim3(1), dim3(64), 0, s, a);
-    if (int e = check_hip(hipGetLastError(), "signal_wait: launch")) return e;
+    // a phase above kMaxFlags: every signal first, then the waits, in
+    // kMaxFlags pieces (a wait must never precede a signal of its phase)
+    for (int i = 0; i < q.nsig; i += kMaxFlags)
+      if (int e = push(q.sig + i, q.nsig - i < kMaxFlags ? q.nsig - i : kMaxFlags, nullptr, 0, q.epoch)) return e;
+    for (int i = 0; i < q.nwait; i += kMaxFlags)
+      if (int e = push(nullptr, 0, q.wait + i, q.nwait - i < kMaxFlags ? q.nwait - i : kMaxFlags, q.epoch))
+        return e;
   }
-  return 0;
+  return launch();
 }
 
 // ---------------------------------------------------------- measurement --

@@ -435,6 +435,7 @@ class Comm {
       enqueue_pipeline(s);
       ran_eager = true;
     }
+    CommBench::flush_signals();
     CommBench::hip_check(hipStreamSynchronize(s), "run: stream sync");
     if (*flags.err) CommBench::die("run", "stream-ordered signal timed out (a peer never signalled)");
   }
@@ -451,6 +452,7 @@ class Comm {
         ++it[i];
       }
     }
+    CommBench::flush_signals();  // (the last step's done tokens)
   }
 
   template <class F>

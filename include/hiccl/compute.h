@@ -140,7 +140,9 @@ class Compute {
 #ifndef HICCL_PORT_HOST
   // Stream-ordered execution: enqueue the step's batched kernel on `s`.
   void launch(hipStream_t s) {
-    if (numcomp) check(hiccl_reduce_plan_enqueue(plan, s), "plan_enqueue");  // the caller syncs the stream
+    if (!numcomp) return;
+    CommBench::flush_signals();  // queued signal/wait steps precede this kernel on the stream
+    check(hiccl_reduce_plan_enqueue(plan, s), "plan_enqueue");  // the caller syncs the stream
   }
 #endif
 

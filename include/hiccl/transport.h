@@ -8,9 +8,11 @@
 //   control plane  MPI (rank/size, handle exchange, completion tokens)
 //   IPC / IPC_get  HIP IPC over xGMI: device allocations exported with
 //                  hipIpcGetMemHandle, opened once per peer allocation,
-//                  moved with hipMemcpyAsync by the writer (IPC, "put") or
-//                  the reader (IPC_get, "get"); ready/done tokens over MPI
-//                  keep a step from overwriting bytes a peer still reads
+//                  moved by one batched copy kernel per step (a HICCL_BYTES
+//                  plan) of the writer (IPC, "put") or the reader (IPC_get,
+//                  "get"); ready/done tokens (MPI messages, or device flags
+//                  in stream-ordered mode) keep a step from overwriting
+//                  bytes a peer still reads
 //   MPI            MPI_Isend/Irecv; device buffers staged through pinned
 //                  host memory (MPICH here is not GPU-aware)
 //   XCCL           RCCL point-to-point (ncclSend/ncclRecv in one group per
@@ -365,13 +367,56 @@ inline double signal_timeout() {
   return t;
 }
 
+// Stream-ordered signalling is queued: consecutive signal/wait steps with
+// nothing else between them on the stream (a step's done tokens and the next
+// step's readies) go out as ONE launch of ordered phases
+// (hiccl_signal_wait_phases) -- the same order of every operation on the
+// stream with fewer kernel boundaries.  flush_signals() must run before
+// anything else is enqueued on that stream and before it is synchronised or
+// its capture ends; every such point of the transport and of HiCCL::Comm
+// calls it.
+struct PendingSignals {
+  struct Phase {
+    std::vector<uint32_t *> sig, wait;
+    uint32_t epoch;
+  };
+  std::vector<Phase> phases;
+  const uint32_t *epoch_dev = nullptr;
+  uint32_t *err = nullptr;
+  hipStream_t stream = nullptr;
+};
+
+inline PendingSignals &pending_signals() {
+  static PendingSignals p;
+  return p;
+}
+
+inline void flush_signals() {
+  PendingSignals &p = pending_signals();
+  if (p.phases.empty()) return;
+  std::vector<hiccl_signal_phase_t> ph(p.phases.size());
+  for (size_t i = 0; i < ph.size(); i++) {
+    ph[i].sig = p.phases[i].sig.data();
+    ph[i].nsig = (int)p.phases[i].sig.size();
+    ph[i].wait = (const uint32_t *const *)p.phases[i].wait.data();
+    ph[i].nwait = (int)p.phases[i].wait.size();
+    ph[i].epoch = p.phases[i].epoch;
+  }
+  int e = hiccl_signal_wait_phases(ph.data(), (int)ph.size(), p.epoch_dev, p.err, signal_timeout(), p.stream);
+  p.phases.clear();
+  if (e) die("hiccl_signal_wait", hiccl_last_error());
+}
+
 // epoch_dev != NULL (graph capture): the epoch used is epoch + *epoch_dev at run time.
 inline void signal_wait(const std::vector<uint32_t *> &sig, const std::vector<uint32_t *> &wait, uint32_t epoch,
                         const uint32_t *epoch_dev, uint32_t *err, hipStream_t stream) {
   if (sig.empty() && wait.empty()) return;
-  int e = hiccl_signal_wait_dev(sig.data(), (int)sig.size(), (const uint32_t *const *)wait.data(), (int)wait.size(),
-                                epoch, epoch_dev, err, signal_timeout(), stream);
-  if (e) die("hiccl_signal_wait", hiccl_last_error());
+  PendingSignals &p = pending_signals();
+  if (!p.phases.empty() && (p.epoch_dev != epoch_dev || p.err != err || p.stream != stream)) flush_signals();
+  p.epoch_dev = epoch_dev;
+  p.err = err;
+  p.stream = stream;
+  p.phases.push_back(PendingSignals::Phase{sig, wait, epoch});
 }
 #endif
 
@@ -544,6 +589,7 @@ class Comm {
       if (!flags) die("transport", "stream-ordered Comm used before bind()");
       enqueue(stream);
       enqueue_tail(stream);  // standalone use (measure): no compute in between
+      flush_signals();
       return;
     }
     if (lib == XCCL) {
@@ -611,6 +657,7 @@ class Comm {
 #ifndef HICCL_PORT_HOST
     setup_gpu();
     if (streamed || lib == XCCL) {
+      flush_signals();
       hip_check(hipStreamSynchronize(stream), "transport stream sync");
       if (flags && *flags->err) die("transport", "stream-ordered signal timed out (peer never signalled)");
       return;
@@ -735,6 +782,7 @@ class Comm {
   // the transport synchronises its stream (or orders it by flags), never a
   // plan's completion event: enqueue without one
   static void launch_plan(hiccl_reduce_plan_t *p, hipStream_t s, const char *what) {
+    flush_signals();  // queued signal/wait steps precede this kernel on the stream
     if (hiccl_reduce_plan_enqueue(p, s)) die(what, hiccl_last_error());
   }
 
@@ -749,6 +797,7 @@ class Comm {
   // rank registers the same transfers in the same order, so each pair's
   // sends and receives match).
   void xccl_group(hipStream_t s) {
+    flush_signals();
     build_plans();
     if (selfplan) launch_plan(selfplan, s, "self copies");
 #ifdef HICCL_WITH_RCCL

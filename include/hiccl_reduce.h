@@ -258,6 +258,23 @@ int hiccl_signal_wait_dev(uint32_t *const *sig, int nsig, const uint32_t *const 
                           uint32_t epoch, const uint32_t *epoch_dev, uint32_t *err, double timeout_s,
                           void *stream);
 int hiccl_counter_add(uint32_t *ctr, uint32_t v, void *stream);
+/* Several signal/wait steps in order, in as few launches as possible (one
+ * 64-lane wave runs up to 8 phases, 64 signal and 64 wait flags): phase p
+ * signals its flags with its epoch, then waits for its flags; phase p + 1
+ * starts after every wait of phase p.  Same effect as one
+ * hiccl_signal_wait_dev per phase, with fewer kernel boundaries on the
+ * stream (the transport merges a step's done tokens with the next step's
+ * readies this way).  A phase with more than 64 flags of a kind signals all
+ * of them before its first wait. */
+typedef struct {
+  uint32_t *const *sig;
+  int nsig;
+  const uint32_t *const *wait;
+  int nwait;
+  uint32_t epoch;
+} hiccl_signal_phase_t;
+int hiccl_signal_wait_phases(const hiccl_signal_phase_t *phases, int nphases, const uint32_t *epoch_dev,
+                             uint32_t *err, double timeout_s, void *stream);
 
 /* ----------------------------------------------------------------------
  * Measurement utilities (bench.py; not part of the reference surface).
