@@ -386,8 +386,10 @@ struct PendingSignals {
   hipStream_t stream = nullptr;
 };
 
+// Per host thread: a pipeline is enqueued (and flushed) by one thread, and
+// pipelines of different threads never share a queue.
 inline PendingSignals &pending_signals() {
-  static PendingSignals p;
+  static thread_local PendingSignals p;
   return p;
 }
 
