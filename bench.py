@@ -155,11 +155,19 @@ def run_c5(world, args, allow_shared=False):
     count = 1 << args.c5_log2count
     out = {"workload": f"C5: all-reduce of {count * world * 4 >> 20} MiB fp32 per rank, {world} ranks, hierarchy "
                        f"{{{hier}}} {{{libs}}}, pipedepth 128 (collectives/main.cpp:151-155)"}
-    modes = (("host", {"HICCL_STREAM_ORDERED": "0"}),
-             ("stream_graph", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "0"}),
-             ("stream_graph_fused", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "1"}))
+    fused = {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "1"}
+    modes = [("host", {"HICCL_STREAM_ORDERED": "0"}, hier, libs),
+             ("stream_graph", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "0"}, hier, libs),
+             ("stream_graph_fused", fused, hier, libs)]
+    if hier != str(world):
+        # not the reference's config: the same all-reduce on one flat IPC
+        # level, every peer over its own xGMI link of the full mesh ({1,4,2}
+        # gives its last level one link per rank; it was laid out for
+        # Frontier's GCD pairs)
+        out["flat_workload"] = f"same, hierarchy {{{world}}} {{ipc}}"
+        modes.append(("flat_stream_graph_fused", fused, str(world), "ipc"))
     deadline = time.perf_counter() + 300.0  # the whole leg: never more than ~5 min of the bench run
-    for name, extra in modes:
+    for name, extra, hier, libs in modes:
         left = int(deadline - time.perf_counter())
         if left < 30:
             out[name] = {"skipped": "time budget of the config-5 leg spent"}

@@ -1,7 +1,7 @@
 """GPU tier: bench.py's config-5 leg (the all-reduce composition run as an
 MPI job by rank 0, collectives/main.cpp:151-155) rehearsed on the box's one
-GPU: 2 ranks share it, so the stream-ordered mode falls back to host-driven;
-both modes must produce the JSON the N > 1 bench line carries and pass the
+GPU: 2 or 4 ranks share it, so the stream-ordered mode falls back to
+host-driven; every mode must produce the JSON the N > 1 bench line carries and pass the
 float-exact known-answer check."""
 import argparse
 import os
@@ -15,13 +15,18 @@ sys.path.insert(0, ROOT)
 pytestmark = pytest.mark.gpu
 
 
-def test_c5_leg_rehearsal_two_ranks_one_gpu():
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_c5_leg_rehearsal_one_gpu(ranks):
+    """4 ranks: hierarchy {1,2,2} {MPI,IPC,IPC} plus the flat {4} {IPC} run."""
     import bench
-    res = bench.run_c5(2, argparse.Namespace(c5_log2count=16, c5_iters=2), allow_shared=True)
+    res = bench.run_c5(ranks, argparse.Namespace(c5_log2count=14, c5_iters=2), allow_shared=True)
     assert "workload" in res, res
-    for mode in ("host", "stream_graph", "stream_graph_fused"):
+    modes = ["host", "stream_graph", "stream_graph_fused"] + (["flat_stream_graph_fused"] if ranks > 2 else [])
+    assert [m for m in res if m.endswith(("host", "fused", "graph"))] == modes
+    for mode in modes:
         r = res[mode]
         assert r.get("kat") == "PASSED", r
-        assert r["ranks"] == 2 and r["pipedepth"] == 128
+        assert r["ranks"] == ranks and r["pipedepth"] == 128
+        assert r["hierarchy"] == (str(ranks) if mode.startswith("flat") or ranks == 2 else f"1,{ranks // 2},2")
         assert r["collective_ms_median"] > 0 and r["algorithmic_GBps_median"] > 0
         assert r["kernel_steps_rank0"] > 0 and r["kernel_ms_per_run_max_rank"] > 0
