@@ -108,6 +108,8 @@ class Comm {
     sch.library = {CommBench::MPI};
     add_fence();  // epoch 0 (comm.h:120-128)
   }
+  Comm(const Comm &) = delete;  // owns its schedule buffers, plans and streams
+  Comm &operator=(const Comm &) = delete;
 
   // ------------------------------------------------------------ setters --
   void set_hierarchy(std::vector<int> hierarchy, std::vector<CommBench::library> library) {
@@ -218,9 +220,10 @@ class Comm {
     if (CommBench::myid == CommBench::printid) print_parameters();
     MPI_Barrier(CommBench::comm_mpi);
     const double t0 = MPI_Wtime();
-    Planner<T> P(CommBench::myid, CommBench::numproc, [](size_t n) {
+    Planner<T> P(CommBench::myid, CommBench::numproc, [this](size_t n) {
       T *p = nullptr;
       CommBench::allocate(p, n);
+      owned.push_back(p);
       return p;
     });
     coll_batch = sch.factorize(P);
@@ -505,14 +508,33 @@ class Comm {
   std::vector<uint32_t> graph_base;
   uint32_t replays = 0;
 
+#endif
+
  public:
+  // The schedule's receive / partial buffers are freed with the communicator
+  // (the reference leaks them).  Every rank's run() has completed, so no
+  // peer still moves bytes into or reads them; a peer's mapping keeps the
+  // memory alive until that peer's transports close it.
   ~Comm() {
+    if (running) pthread_join(thread, nullptr);  // a start() without wait(): finish it first
+#ifndef HICCL_PORT_HOST
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph_ctr) (void)hipFree(graph_ctr);
+    if (!owned.empty() || !command_batch.empty()) (void)hipDeviceSynchronize();
+#endif
+    // the steps' transports (closing their IPC mappings) and computes (the
+    // reference never deletes them)
+    for (auto &lst : command_batch)
+      for (auto &c : lst) {
+        delete c.comm;
+        delete c.compute;
+      }
+    command_batch.clear();
+    for (T *p : owned) CommBench::free(p);
   }
 
  private:
-#endif
+  std::vector<T *> owned;  // allocated by init() for the schedule
 
   bool want_graph() {
 #ifdef HICCL_PORT_HOST

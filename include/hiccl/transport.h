@@ -291,8 +291,17 @@ struct IpcExport {
   uint64_t offset;  // byte offset of the buffer inside that allocation
 };
 
-inline std::map<IpcKey, char *> &ipc_opened() {
-  static std::map<IpcKey, char *> m;
+// Mappings are reference-counted per holder (a transport, a flag space) and
+// closed with the last holder: a peer that frees an allocation and gets the
+// same base address again for a new one (the next communicator's buffers)
+// must never be reached through the old mapping.
+struct IpcMapping {
+  char *ptr;
+  int refs;
+};
+
+inline std::map<IpcKey, IpcMapping> &ipc_opened() {
+  static std::map<IpcKey, IpcMapping> m;
   return m;
 }
 
@@ -308,16 +317,33 @@ inline IpcExport ipc_export(const void *p) {
   return e;
 }
 
-inline char *ipc_import(int peer, const IpcExport &e) {
+// The mapping of peer's exported buffer; its key is appended to `held`,
+// which the holder hands to ipc_release when it no longer uses the mapping.
+inline char *ipc_import(int peer, const IpcExport &e, std::vector<IpcKey> &held) {
   IpcKey k{peer, (uintptr_t)e.base};
   auto &m = ipc_opened();
   auto it = m.find(k);
   if (it == m.end()) {
     void *ptr = nullptr;
     hip_check(hipIpcOpenMemHandle(&ptr, e.handle, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-    it = m.emplace(k, (char *)ptr).first;
+    it = m.emplace(k, IpcMapping{(char *)ptr, 0}).first;
   }
-  return it->second + e.offset;
+  it->second.refs++;
+  held.push_back(k);
+  return it->second.ptr + e.offset;
+}
+
+inline void ipc_release(std::vector<IpcKey> &held) {
+  auto &m = ipc_opened();
+  for (const IpcKey &k : held) {
+    auto it = m.find(k);
+    if (it == m.end()) continue;
+    if (--it->second.refs == 0) {
+      (void)hipIpcCloseMemHandle(it->second.ptr);
+      m.erase(it);
+    }
+  }
+  held.clear();
 }
 
 // A communicator's flag array: one uint32 per slot in device memory on every
@@ -329,6 +355,7 @@ struct FlagSpace {
   std::vector<uint32_t *> peer;  // peer[r]: rank r's array as mapped here (peer[myid] = local)
   size_t nflags = 0;
   uint32_t *err = nullptr;
+  std::vector<IpcKey> held;  // peers' flag arrays mapped here
 
   // Collective over comm_mpi.
   // The flags are uncached device memory (hipDeviceMallocUncached): a peer
@@ -348,9 +375,10 @@ struct FlagSpace {
     mpi_check(MPI_Allgather(&mine, sizeof(IpcExport), MPI_BYTE, all.data(), sizeof(IpcExport), MPI_BYTE, comm_mpi),
               "MPI_Allgather(flags)");
     peer.assign(numproc, nullptr);
-    for (int r = 0; r < numproc; r++) peer[r] = r == myid ? local : (uint32_t *)ipc_import(r, all[r]);
+    for (int r = 0; r < numproc; r++) peer[r] = r == myid ? local : (uint32_t *)ipc_import(r, all[r], held);
   }
   ~FlagSpace() {
+    ipc_release(held);
     if (err) (void)hipHostFree(err);
     if (local) (void)hipFree(local);
   }
@@ -461,10 +489,12 @@ class Comm {
 
   ~Comm() {
 #ifndef HICCL_PORT_HOST
+    if (!held.empty()) (void)hipStreamSynchronize(stream);  // no copy still reads or writes a mapping
     for (auto &x : xfers)
       if (x.staging) (void)hipHostFree(x.staging);
     if (moveplan) hiccl_reduce_plan_destroy(moveplan);
     if (selfplan) hiccl_reduce_plan_destroy(selfplan);
+    ipc_release(held);
 #endif
   }
 
@@ -509,7 +539,7 @@ class Comm {
       if (myid == mover) {
         IpcExport e;
         mpi_check(MPI_Recv(&e, sizeof(e), MPI_BYTE, owner, x.tag, comm_mpi, MPI_STATUS_IGNORE), "MPI_Recv(ipc)");
-        x.remote = ipc_import(owner, e);
+        x.remote = ipc_import(owner, e, held);
       }
     }
     if (sendid != recvid && lib == MPI && (myid == sendid || myid == recvid))
@@ -754,6 +784,7 @@ class Comm {
   hipStream_t stream = nullptr;
   bool streamed = false;
   FlagSpace *flags = nullptr;
+  std::vector<IpcKey> held;  // the owners' buffers this rank maps (ipc_import)
   uint32_t epoch = 0;
   const uint32_t *graph_epoch = nullptr;  // set while a graph is being captured
   uint32_t sig_epoch() const { return graph_epoch ? epoch - 1 : epoch; }

@@ -132,9 +132,12 @@ def test_known_answer_graph_replay(np_, hier, libs, pattern):
 @pytest.mark.parametrize("streamed", [True, False], ids=["stream", "host"])
 @pytest.mark.parametrize("np_", [2, 4])
 def test_readme_api_example(np_, streamed):
-    rc, out = mpirun(np_, os.path.join(ROOT, "build", "readme_example_hip"), [250000, 3], streamed=streamed)
+    """Three rounds, each with a fresh communicator and fresh user buffers
+    (the previous round's freed first): peers' new buffers often get the
+    freed addresses, which must not be reached through a stale IPC mapping."""
+    rc, out = mpirun(np_, os.path.join(ROOT, "build", "readme_example_hip"), [250000, 3, 3], streamed=streamed)
     assert rc == 0, out[-3000:]
-    assert "README all-reduce: PASSED" in out
+    assert out.count("README all-reduce: PASSED") == 3, out[-3000:]
 
 
 @pytest.mark.parametrize("pattern", [8, 7])
