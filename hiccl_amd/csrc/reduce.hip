@@ -34,6 +34,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -1329,7 +1330,20 @@ struct hiccl_reduce_plan {
   hipStream_t own = nullptr;
   hipStream_t last = nullptr;  // stream of the last launch (plan_sync synchronises it)
   bool launched = false;
+  std::atomic<bool> enqueued{false};  // some launch went out (on a stream not remembered)
 };
+
+namespace {
+// Before the plan's device block is freed: no launch may still read it.
+void plan_quiesce(hiccl_reduce_plan *p) {
+  if (p->enqueued.load(std::memory_order_relaxed)) {
+    (void)hipDeviceSynchronize();
+    p->enqueued.store(false, std::memory_order_relaxed);
+  } else if (p->launched) {
+    (void)hipStreamSynchronize(p->last);
+  }
+}
+}  // namespace
 
 namespace {
 
@@ -1363,7 +1377,7 @@ int plan_upload(hiccl_reduce_plan *p, hipStream_t s) {
     return fail(hipErrorStreamCaptureUnsupported,
                 "plan: the first launch after an add or a config change uploads the plan and cannot be captured");
   if (p->d_block) {
-    if (p->launched) (void)hipStreamSynchronize(p->last);  // a running launch still reads it
+    plan_quiesce(p);  // a running launch still reads it
     (void)hipFree(p->d_block);
     p->d_block = nullptr;
   }
@@ -1576,15 +1590,20 @@ int hiccl_reduce_plan_enqueue(hiccl_reduce_plan_t *p, void *stream) {
   if (p->comps.empty()) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (int e = plan_upload(p, s)) return e;
-  return plan_kernel(p, s);
+  if (int e = plan_kernel(p, s)) return e;
+  // no stream bookkeeping (callers on several threads and streams); a
+  // re-upload or destroy then synchronises the device before it frees the
+  // block a launch may still read
+  p->enqueued.store(true, std::memory_order_relaxed);
+  return 0;
 }
 
 int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *p, void *stream) {
   if (int e = hiccl_reduce_plan_enqueue(p, stream)) return e;
   if (p->comps.empty()) return 0;
   hipStream_t s = (hipStream_t)stream;
-  // a capturing stream gets no completion event (plan_sync does not apply
-  // to graph replays: synchronise the stream the graph runs on)
+  // a capturing stream is not remembered (plan_sync does not apply to graph
+  // replays: synchronise the stream the graph runs on)
   if (capturing(s, false)) return 0;
   p->launched = true;
   p->last = s;
@@ -1636,7 +1655,8 @@ size_t hiccl_reduce_plan_bytes(const hiccl_reduce_plan_t *p) {
 void hiccl_reduce_plan_destroy(hiccl_reduce_plan_t *p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
-  if (p->launched) (void)hipStreamSynchronize(p->last);
+  if (p->d_block) plan_quiesce(p);
+  else if (p->launched) (void)hipStreamSynchronize(p->last);
   if (p->d_block) (void)hipFree(p->d_block);
   if (p->own) (void)hipStreamDestroy(p->own);
   delete p;

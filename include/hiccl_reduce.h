@@ -191,7 +191,10 @@ int hiccl_reduce_plan_add(hiccl_reduce_plan_t *plan, void *out, const void *cons
 int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *plan, void *stream);
 /* launch without remembering the stream for hiccl_reduce_plan_sync: for
  * stream-ordered callers that synchronise the stream themselves, and for
- * launches from several threads onto different streams. */
+ * launches from several threads onto different streams.  A later re-upload
+ * (the first launch after an add or a config change) or destroy of a plan
+ * launched this way synchronises the device before it frees the plan's
+ * device table. */
 int hiccl_reduce_plan_enqueue(hiccl_reduce_plan_t *plan, void *stream);
 /* Reference structure, for measurement: one kernel per compute, each on
  * the given stream (compute.h:88-91 launches one kernel per compute) --
