@@ -13,9 +13,9 @@ import torch
 from . import _lib as L
 
 
-def _stream_handle(stream):
+def _stream_handle(stream, device=None):
     if stream is None:
-        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
     if isinstance(stream, int):
         return ctypes.c_void_p(stream)
     return ctypes.c_void_p(stream.cuda_stream)
@@ -55,10 +55,14 @@ def reduce(out, inputs, count=None, stream=None, config=None):
     _check_tensor(out, "out")
     if count is None:
         count = out.numel()
+    if count < 0:
+        raise ValueError(f"hiccl: count={count} < 0")
     dt = _dtype_code(out)
     ptrs = []
     for k, x in enumerate(inputs):
         _check_tensor(x, f"inputs[{k}]")
+        if x.device != out.device:
+            raise ValueError(f"hiccl: inputs[{k}] is on {x.device}, out on {out.device}")
         if x.dtype != out.dtype:
             raise TypeError(f"hiccl: inputs[{k}] dtype {x.dtype} != out dtype {out.dtype}")
         if x.numel() < count:
@@ -67,13 +71,14 @@ def reduce(out, inputs, count=None, stream=None, config=None):
     if out.numel() < count:
         raise ValueError(f"hiccl: out has {out.numel()} < count={count} elements")
     tab = _ptr_table(ptrs)
-    s = _stream_handle(stream)
-    if config is None:
-        rc = L.lib().hiccl_reduce(dt, ctypes.c_void_p(out.data_ptr()), tab, len(ptrs), count, s)
-    else:
-        cfg = L.ReduceConfig(**config)
-        rc = L.lib().hiccl_reduce_ex(dt, ctypes.c_void_p(out.data_ptr()), tab, len(ptrs), count, s,
-                                     ctypes.byref(cfg))
+    with torch.cuda.device(out.device):  # the library launches on the current device
+        s = _stream_handle(stream, out.device)
+        if config is None:
+            rc = L.lib().hiccl_reduce(dt, ctypes.c_void_p(out.data_ptr()), tab, len(ptrs), count, s)
+        else:
+            cfg = L.ReduceConfig(**config)
+            rc = L.lib().hiccl_reduce_ex(dt, ctypes.c_void_p(out.data_ptr()), tab, len(ptrs), count, s,
+                                         ctypes.byref(cfg))
     L.check(rc, "hiccl_reduce")
     return out
 
@@ -175,15 +180,15 @@ class Compute:
             own.wait_stream(torch.cuda.current_stream(self.device))
             s = ctypes.c_void_p(self.stream_handle())
         else:
-            s = _stream_handle(stream)
+            s = _stream_handle(stream, self.device)
         fn = L.lib().hiccl_reduce_plan_launch_each if each else L.lib().hiccl_reduce_plan_launch
         L.check(fn(self._plan, s), "plan_launch")
 
     def enqueue(self, stream=None):
-        """Launch on ``stream`` (default torch's current stream) without the
-        completion event :meth:`wait` uses (hiccl_reduce_plan_enqueue): for
+        """Launch on ``stream`` (default torch's current stream) without
+        remembering it for :meth:`wait` (hiccl_reduce_plan_enqueue): for
         stream-ordered pipelines that synchronise the stream themselves."""
-        L.check(L.lib().hiccl_reduce_plan_enqueue(self._plan, _stream_handle(stream)), "plan_enqueue")
+        L.check(L.lib().hiccl_reduce_plan_enqueue(self._plan, _stream_handle(stream, self.device)), "plan_enqueue")
 
     def wait(self):
         L.check(L.lib().hiccl_reduce_plan_sync(self._plan), "plan_sync")

@@ -260,6 +260,16 @@ def test_phase_unsupported_shape_is_an_error():
         hiccl_amd.reduce(x, [x, x], config=dict(schedule=9))
 
 
+def test_python_reduce_argument_checks():
+    x = torch.zeros(100, device=DEV)
+    with pytest.raises(ValueError, match="count"):
+        hiccl_amd.reduce(x, [x], count=-1)
+    with pytest.raises(ValueError, match="device tensor"):
+        hiccl_amd.reduce(x, [x.cpu()])
+    with pytest.raises(ValueError, match="< count"):
+        hiccl_amd.reduce(x, [x[:50]], count=100)
+
+
 @pytest.mark.parametrize("config", [
     dict(block=256, unroll=1), dict(block=256, unroll=2), dict(block=256, unroll=4),
     dict(block=512, unroll=1), dict(block=512, unroll=2), dict(block=512, unroll=4),
