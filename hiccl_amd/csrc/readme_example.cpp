@@ -33,6 +33,10 @@ int main(int argc, char **argv) {
     T *recvbuf;
     allocate(sendbuf, count * numproc);
     allocate(recvbuf, count * numproc);
+    if (std::getenv("HICCL_README_TOUCH")) {  // diagnostic: this rank writes its recvbuf once before any peer
+      std::vector<T> zero(count * numproc, (T)0);
+      CommBench::memcpyH2D(recvbuf, zero.data(), zero.size());
+    }
 
     // partial reductions (each GPU gathers count elements from all GPUs for reduction)
     for (int i = 0; i < numproc; i++) allreduce.add_reduction(sendbuf + i * count, recvbuf + i * count, count, HiCCL::all, i);
@@ -68,7 +72,12 @@ int main(int argc, char **argv) {
     const double ranks = (double)numproc * (numproc + 1) / 2 + (double)round * numproc;
     size_t errors = 0;
     for (size_t i = 0; i < out.size(); i++)
-      if (out[i] != (T)(ranks * ((i % 7) + 1))) errors++;
+      if (out[i] != (T)(ranks * ((i % 7) + 1))) {
+        if (!errors)
+          std::printf("rank %d round %d: first wrong element %zu (chunk %zu): %g, want %g\n", myid, round, i, i / count,
+                      (double)out[i], ranks * ((i % 7) + 1));
+        errors++;
+      }
     unsigned long total = errors;
     MPI_Allreduce(MPI_IN_PLACE, &total, 1, MPI_UNSIGNED_LONG, MPI_SUM, comm_mpi);
     if (myid == 0) std::printf("README all-reduce: %s (%lu errors, %d ranks, count %zu, round %d)\n", total ? "FAILED" : "PASSED", total, numproc, count, round);

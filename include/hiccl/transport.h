@@ -305,6 +305,15 @@ inline std::map<IpcKey, IpcMapping> &ipc_opened() {
   return m;
 }
 
+// HICCL_DEBUG_IPC=1: every export, import and close on stdout.
+inline bool ipc_debug() {
+  static const bool on = [] {
+    const char *e = std::getenv("HICCL_DEBUG_IPC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 inline IpcExport ipc_export(const void *p) {
   IpcExport e;
   std::memset(&e, 0, sizeof(e));
@@ -314,6 +323,9 @@ inline IpcExport ipc_export(const void *p) {
   hip_check(hipIpcGetMemHandle(&e.handle, (void *)base), "hipIpcGetMemHandle");
   e.base = (uint64_t)(uintptr_t)base;
   e.offset = (uint64_t)((const char *)p - (const char *)base);
+  if (ipc_debug())
+    std::printf("[ipc %d] export %p = base %p + %llu (size %zu)\n", myid, p, (void *)base,
+                (unsigned long long)e.offset, size);
   return e;
 }
 
@@ -330,6 +342,10 @@ inline char *ipc_import(int peer, const IpcExport &e, std::vector<IpcKey> &held)
   }
   it->second.refs++;
   held.push_back(k);
+  if (ipc_debug())
+    std::printf("[ipc %d] import peer %d base %#llx + %llu -> %p (refs %d)\n", myid, peer,
+                (unsigned long long)e.base, (unsigned long long)e.offset, (void *)(it->second.ptr + e.offset),
+                it->second.refs);
   return it->second.ptr + e.offset;
 }
 
@@ -339,6 +355,9 @@ inline void ipc_release(std::vector<IpcKey> &held) {
     auto it = m.find(k);
     if (it == m.end()) continue;
     if (--it->second.refs == 0) {
+      if (ipc_debug())
+        std::printf("[ipc %d] close peer %d base %#llx at %p\n", myid, k.rank, (unsigned long long)k.base,
+                    (void *)it->second.ptr);
       (void)hipIpcCloseMemHandle(it->second.ptr);
       m.erase(it);
     }
