@@ -82,6 +82,9 @@ int main(int argc, char **argv) {
     MPI_Allreduce(MPI_IN_PLACE, &total, 1, MPI_UNSIGNED_LONG, MPI_SUM, comm_mpi);
     if (myid == 0) std::printf("README all-reduce: %s (%lu errors, %d ranks, count %zu, round %d)\n", total ? "FAILED" : "PASSED", total, numproc, count, round);
     failed += total;
+#ifndef HICCL_PORT_HOST
+    if (total) CommBench::ipc_log_dump();  // HICCL_DEBUG_IPC=2
+#endif
     free(sendbuf);
     free(recvbuf);
   }

@@ -305,13 +305,29 @@ inline std::map<IpcKey, IpcMapping> &ipc_opened() {
   return m;
 }
 
-// HICCL_DEBUG_IPC=1: every export, import and close on stdout.
-inline bool ipc_debug() {
-  static const bool on = [] {
+// HICCL_DEBUG_IPC=1: every export, import and close on stdout; =2: kept in
+// memory (timing barely changes) and printed by ipc_log_dump().
+inline int ipc_debug() {
+  static const int on = [] {
     const char *e = std::getenv("HICCL_DEBUG_IPC");
-    return e && e[0] == '1';
+    return e ? std::atoi(e) : 0;
   }();
   return on;
+}
+inline std::string &ipc_log() {
+  static std::string s;
+  return s;
+}
+template <typename... A>
+void ipc_note(const char *fmt, A... a) {
+  char line[256];
+  std::snprintf(line, sizeof(line), fmt, a...);
+  if (ipc_debug() == 1) std::fputs(line, stdout);
+  else ipc_log() += line;
+}
+inline void ipc_log_dump() {
+  std::fputs(ipc_log().c_str(), stdout);
+  std::fflush(stdout);
 }
 
 inline IpcExport ipc_export(const void *p) {
@@ -324,8 +340,8 @@ inline IpcExport ipc_export(const void *p) {
   e.base = (uint64_t)(uintptr_t)base;
   e.offset = (uint64_t)((const char *)p - (const char *)base);
   if (ipc_debug())
-    std::printf("[ipc %d] export %p = base %p + %llu (size %zu)\n", myid, p, (void *)base,
-                (unsigned long long)e.offset, size);
+    ipc_note("[ipc %d] export %p = base %p + %llu (size %zu)\n", myid, p, (void *)base, (unsigned long long)e.offset,
+             size);
   return e;
 }
 
@@ -343,7 +359,7 @@ inline char *ipc_import(int peer, const IpcExport &e, std::vector<IpcKey> &held)
   it->second.refs++;
   held.push_back(k);
   if (ipc_debug())
-    std::printf("[ipc %d] import peer %d base %#llx + %llu -> %p (refs %d)\n", myid, peer,
+    ipc_note("[ipc %d] import peer %d base %#llx + %llu -> %p (refs %d)\n", myid, peer,
                 (unsigned long long)e.base, (unsigned long long)e.offset, (void *)(it->second.ptr + e.offset),
                 it->second.refs);
   return it->second.ptr + e.offset;
@@ -355,9 +371,16 @@ inline void ipc_release(std::vector<IpcKey> &held) {
     auto it = m.find(k);
     if (it == m.end()) continue;
     if (--it->second.refs == 0) {
+      static const bool keep = std::getenv("HICCL_IPC_KEEP_OPEN") != nullptr;  // diagnostic only
+      if (keep) {
+        if (ipc_debug()) ipc_note("[ipc %d] keep open peer %d base %#llx at %p\n", myid, k.rank,
+                                  (unsigned long long)k.base, (void *)it->second.ptr);
+        m.erase(it);
+        continue;
+      }
       if (ipc_debug())
-        std::printf("[ipc %d] close peer %d base %#llx at %p\n", myid, k.rank, (unsigned long long)k.base,
-                    (void *)it->second.ptr);
+        ipc_note("[ipc %d] close peer %d base %#llx at %p\n", myid, k.rank, (unsigned long long)k.base,
+                 (void *)it->second.ptr);
       (void)hipIpcCloseMemHandle(it->second.ptr);
       m.erase(it);
     }
@@ -557,7 +580,12 @@ class Comm {
       }
       if (myid == mover) {
         IpcExport e;
-        mpi_check(MPI_Recv(&e, sizeof(e), MPI_BYTE, owner, x.tag, comm_mpi, MPI_STATUS_IGNORE), "MPI_Recv(ipc)");
+        std::memset(&e, 0, sizeof(e));
+        MPI_Status st;
+        mpi_check(MPI_Recv(&e, sizeof(e), MPI_BYTE, owner, x.tag, comm_mpi, &st), "MPI_Recv(ipc)");
+        int got = 0;
+        MPI_Get_count(&st, MPI_BYTE, &got);
+        if (got != (int)sizeof(e)) die("transport", "IPC handle exchange matched a message of " + std::to_string(got) + " bytes");
         x.remote = ipc_import(owner, e, held);
       }
     }
@@ -827,6 +855,9 @@ class Comm {
       const void *src = self || lib == IPC ? (const void *)x.src : (const void *)x.remote;
       void *dst = self || lib == IPC_get ? (void *)x.dst : (void *)x.remote;
       if (lib == IPC && !self) dst = x.remote;
+      if (ipc_debug())
+        ipc_note("[ipc %d] %s copy %p -> %p, %zu B (transfer %d -> %d)\n", myid, self ? "self" : "move", src, dst,
+                 x.count * sizeof(T), x.sendid, x.recvid);
       if (hiccl_reduce_plan_add(p, dst, &src, 1, x.count * sizeof(T))) die("transport copy plan", hiccl_last_error());
     }
   }
