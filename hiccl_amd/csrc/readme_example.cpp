@@ -27,8 +27,6 @@ int main(int argc, char **argv) {
   const int rounds = argc > 3 ? std::atoi(argv[3]) : 1;
   unsigned long failed = 0;
   for (int round = 0; round < rounds; round++) {
-    Comm<T> allreduce;
-
     T *sendbuf;
     T *recvbuf;
     allocate(sendbuf, count * numproc);
@@ -38,53 +36,59 @@ int main(int argc, char **argv) {
       CommBench::memcpyH2D(recvbuf, zero.data(), zero.size());
     }
 
-    // partial reductions (each GPU gathers count elements from all GPUs for reduction)
-    for (int i = 0; i < numproc; i++) allreduce.add_reduction(sendbuf + i * count, recvbuf + i * count, count, HiCCL::all, i);
-    // express ordering of the primitives
-    allreduce.add_fence();
-    // multicast partial results (each GPU sends count elements to all GPUs except itself)
-    for (int i = 0; i < numproc; i++)
-      allreduce.add_multicast(recvbuf + i * count, recvbuf + i * count, count, i, HiCCL::others);
+    // the communicator goes before its buffers: a peer must close its IPC mapping
+    // of a buffer before the owner frees it (hipIpcOpenMemHandle: UB otherwise)
+    {
+      Comm<T> allreduce;
 
-    // optimization parameters: two-level hierarchy when the rank count allows
-    std::vector<int> hierarchy = {numproc};
-    std::vector<library> lib = {IPC};
-    if (numproc % 2 == 0 && numproc > 2) {
-      hierarchy = {numproc / 2, 2};
-      lib = {MPI, IPC};
-    }
-    int numstripe(1);  // multi-rail striping (off)
-    int ring(1);       // number of virtual ring nodes (off)
-    int pipeline(4);   // pipeline depth
-    allreduce.init(hierarchy, lib, numstripe, ring, pipeline);
+      // partial reductions (each GPU gathers count elements from all GPUs for reduction)
+      for (int i = 0; i < numproc; i++) allreduce.add_reduction(sendbuf + i * count, recvbuf + i * count, count, HiCCL::all, i);
+      // express ordering of the primitives
+      allreduce.add_fence();
+      // multicast partial results (each GPU sends count elements to all GPUs except itself)
+      for (int i = 0; i < numproc; i++)
+        allreduce.add_multicast(recvbuf + i * count, recvbuf + i * count, count, i, HiCCL::others);
 
-    std::vector<T> host(count * numproc);
-    for (size_t i = 0; i < host.size(); i++) host[i] = (T)((myid + 1 + round) * ((i % 7) + 1));
-    CommBench::memcpyH2D(sendbuf, host.data(), host.size());
-
-    for (int iter = 0; iter < numiter; iter++) {
-      allreduce.start();  // nonblocking start
-      allreduce.wait();   // blocking wait
-    }
-
-    std::vector<T> out(count * numproc);
-    CommBench::memcpyD2H(out.data(), recvbuf, out.size());
-    const double ranks = (double)numproc * (numproc + 1) / 2 + (double)round * numproc;
-    size_t errors = 0;
-    for (size_t i = 0; i < out.size(); i++)
-      if (out[i] != (T)(ranks * ((i % 7) + 1))) {
-        if (!errors)
-          std::printf("rank %d round %d: first wrong element %zu (chunk %zu): %g, want %g\n", myid, round, i, i / count,
-                      (double)out[i], ranks * ((i % 7) + 1));
-        errors++;
+      // optimization parameters: two-level hierarchy when the rank count allows
+      std::vector<int> hierarchy = {numproc};
+      std::vector<library> lib = {IPC};
+      if (numproc % 2 == 0 && numproc > 2) {
+        hierarchy = {numproc / 2, 2};
+        lib = {MPI, IPC};
       }
-    unsigned long total = errors;
-    MPI_Allreduce(MPI_IN_PLACE, &total, 1, MPI_UNSIGNED_LONG, MPI_SUM, comm_mpi);
-    if (myid == 0) std::printf("README all-reduce: %s (%lu errors, %d ranks, count %zu, round %d)\n", total ? "FAILED" : "PASSED", total, numproc, count, round);
-    failed += total;
+      int numstripe(1);  // multi-rail striping (off)
+      int ring(1);       // number of virtual ring nodes (off)
+      int pipeline(4);   // pipeline depth
+      allreduce.init(hierarchy, lib, numstripe, ring, pipeline);
+
+      std::vector<T> host(count * numproc);
+      for (size_t i = 0; i < host.size(); i++) host[i] = (T)((myid + 1 + round) * ((i % 7) + 1));
+      CommBench::memcpyH2D(sendbuf, host.data(), host.size());
+
+      for (int iter = 0; iter < numiter; iter++) {
+        allreduce.start();  // nonblocking start
+        allreduce.wait();   // blocking wait
+      }
+
+      std::vector<T> out(count * numproc);
+      CommBench::memcpyD2H(out.data(), recvbuf, out.size());
+      const double ranks = (double)numproc * (numproc + 1) / 2 + (double)round * numproc;
+      size_t errors = 0;
+      for (size_t i = 0; i < out.size(); i++)
+        if (out[i] != (T)(ranks * ((i % 7) + 1))) {
+          if (!errors)
+            std::printf("rank %d round %d: first wrong element %zu (chunk %zu): %g, want %g\n", myid, round, i, i / count,
+                        (double)out[i], ranks * ((i % 7) + 1));
+          errors++;
+        }
+      unsigned long total = errors;
+      MPI_Allreduce(MPI_IN_PLACE, &total, 1, MPI_UNSIGNED_LONG, MPI_SUM, comm_mpi);
+      if (myid == 0) std::printf("README all-reduce: %s (%lu errors, %d ranks, count %zu, round %d)\n", total ? "FAILED" : "PASSED", total, numproc, count, round);
+      failed += total;
 #ifndef HICCL_PORT_HOST
-    if (total) CommBench::ipc_log_dump();  // HICCL_DEBUG_IPC=2
+      if (total) CommBench::ipc_log_dump();  // HICCL_DEBUG_IPC=2
 #endif
+    }
     free(sendbuf);
     free(recvbuf);
   }

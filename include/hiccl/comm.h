@@ -512,9 +512,13 @@ class Comm {
 
  public:
   // The schedule's receive / partial buffers are freed with the communicator
-  // (the reference leaks them).  Every rank's run() has completed, so no
-  // peer still moves bytes into or reads them; a peer's mapping keeps the
-  // memory alive until that peer's transports close it.
+  // (the reference leaks them).  Collective: every rank first closes its IPC
+  // mappings of its peers' buffers (deleting the transports), then a barrier,
+  // then the buffers are freed -- HIP leaves freeing an exported allocation
+  // that another process still has open undefined (hipIpcOpenMemHandle), and
+  // on MI355X it loses writes made through the peer's next mapping of that
+  // address.  The same order is the caller's duty for its own buffers:
+  // destroy the communicator before freeing what it was built on.
   ~Comm() {
     if (running) pthread_join(thread, nullptr);  // a start() without wait(): finish it first
 #ifndef HICCL_PORT_HOST
@@ -530,6 +534,12 @@ class Comm {
         delete c.compute;
       }
     command_batch.clear();
+#ifndef HICCL_PORT_HOST
+    flags.close();  // peers' flag arrays
+    int fin = 0;
+    MPI_Finalized(&fin);
+    if (!fin) MPI_Barrier(CommBench::comm_mpi);  // every peer's mappings of this rank's buffers are closed
+#endif
     for (T *p : owned) CommBench::free(p);
   }
 

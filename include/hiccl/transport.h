@@ -419,6 +419,8 @@ struct FlagSpace {
     peer.assign(numproc, nullptr);
     for (int r = 0; r < numproc; r++) peer[r] = r == myid ? local : (uint32_t *)ipc_import(r, all[r], held);
   }
+  // Close the mappings of the peers' arrays (before the peers free them).
+  void close() { ipc_release(held); }
   ~FlagSpace() {
     ipc_release(held);
     if (err) (void)hipHostFree(err);
