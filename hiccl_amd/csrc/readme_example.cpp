@@ -26,11 +26,15 @@ int main(int argc, char **argv) {
   // previous round's are freed: a peer's new buffer may get the same address)
   const int rounds = argc > 3 ? std::atoi(argv[3]) : 1;
   unsigned long failed = 0;
+  // HICCL_README_KEEP_BUFFERS (diagnostic): one pair of user buffers for all rounds
+  const bool keep = std::getenv("HICCL_README_KEEP_BUFFERS") != nullptr;
+  T *sendbuf = nullptr;
+  T *recvbuf = nullptr;
   for (int round = 0; round < rounds; round++) {
-    T *sendbuf;
-    T *recvbuf;
-    allocate(sendbuf, count * numproc);
-    allocate(recvbuf, count * numproc);
+    if (!keep || round == 0) {
+      allocate(sendbuf, count * numproc);
+      allocate(recvbuf, count * numproc);
+    }
     if (std::getenv("HICCL_README_TOUCH")) {  // diagnostic: this rank writes its recvbuf once before any peer
       std::vector<T> zero(count * numproc, (T)0);
       CommBench::memcpyH2D(recvbuf, zero.data(), zero.size());
@@ -89,8 +93,10 @@ int main(int argc, char **argv) {
       if (total) CommBench::ipc_log_dump();  // HICCL_DEBUG_IPC=2
 #endif
     }
-    free(sendbuf);
-    free(recvbuf);
+    if (!keep || round == rounds - 1) {
+      free(sendbuf);
+      free(recvbuf);
+    }
   }
   MPI_Finalize();
   return failed ? 1 : 0;

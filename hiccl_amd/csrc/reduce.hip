@@ -841,7 +841,9 @@ uint32_t *unit_sched_for(int engine, double n, uint64_t units, uint64_t grid, in
   if (it != g_sched.end()) return it->second;
   uint32_t *p = nullptr;
   if (hipMalloc((void **)&p, 64) != hipSuccess) return nullptr;
-  if (hipMemset(p, 0, 64) != hipSuccess) {
+  // zeroed in order on `s` (a null-stream memset does not order a
+  // non-blocking stream's first kernel after it)
+  if (hipMemsetAsync(p, 0, 64, s) != hipSuccess) {
     (void)hipFree(p);
     return nullptr;
   }

@@ -11,5 +11,5 @@ for i in $(seq "$runs"); do
   rc=$?
   fails=$(grep -c FAILED <<< "$out")
   echo "run $i rc=$rc failed_rounds=$fails"
-  if [ $rc -ne 0 ]; then echo "$out" > gpurun_out/readme_fail.txt; grep -E "wrong|FAILED|hiccl" <<< "$out" | head -20; exit $rc; fi
+  if [ $rc -ne 0 ]; then echo "$out" > "gpurun_out/readme_fail_$$.txt"; grep -E "wrong|FAILED|hiccl" <<< "$out" | head -20; exit $rc; fi
 done
