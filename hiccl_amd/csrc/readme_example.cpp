@@ -75,7 +75,17 @@ int main(int argc, char **argv) {
       }
 
       std::vector<T> out(count * numproc);
-      CommBench::memcpyD2H(out.data(), recvbuf, out.size());
+#ifndef HICCL_PORT_HOST
+      if (std::getenv("HICCL_README_KERNEL_READ")) {  // diagnostic: read back through a kernel copy
+        T *tmp = nullptr;
+        allocate(tmp, out.size());
+        if (hiccl_stream_copy(tmp, recvbuf, out.size() * sizeof(T), nullptr)) CommBench::die("copy", "");
+        CommBench::hip_check(hipDeviceSynchronize(), "sync");
+        CommBench::memcpyD2H(out.data(), tmp, out.size());
+        free(tmp);
+      } else
+#endif
+        CommBench::memcpyD2H(out.data(), recvbuf, out.size());
       const double ranks = (double)numproc * (numproc + 1) / 2 + (double)round * numproc;
       size_t errors = 0;
       for (size_t i = 0; i < out.size(); i++)
@@ -93,7 +103,7 @@ int main(int argc, char **argv) {
       if (total) CommBench::ipc_log_dump();  // HICCL_DEBUG_IPC=2
 #endif
     }
-    if (!keep || round == rounds - 1) {
+    if ((!keep || round == rounds - 1) && !std::getenv("HICCL_README_NOFREE")) {  // NOFREE: diagnostic leak
       free(sendbuf);
       free(recvbuf);
     }

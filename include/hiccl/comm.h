@@ -266,7 +266,6 @@ class Comm {
           base += c.comm->size();
         }
     }
-    CommBench::ipc_close_retired();  // (HICCL_IPC_CLOSE=defer) after this communicator's imports
 #endif
     buffsize = P.buffsize;
     recycle = P.recycle;

@@ -298,7 +298,6 @@ struct IpcExport {
 struct IpcMapping {
   char *ptr;
   int refs;
-  size_t size;  // of the mapped range (hipMemGetAddressRange)
 };
 
 inline std::map<IpcKey, IpcMapping> &ipc_opened() {
@@ -330,6 +329,12 @@ inline void ipc_log_dump() {
   std::fputs(ipc_log().c_str(), stdout);
   std::fflush(stdout);
 }
+inline unsigned long long handle_hash(const hipIpcMemHandle_t &h) {  // FNV-1a of the handle bytes
+  const unsigned char *b = reinterpret_cast<const unsigned char *>(&h);
+  unsigned long long x = 1469598103934665603ull;
+  for (size_t i = 0; i < sizeof(h); i++) x = (x ^ b[i]) * 1099511628211ull;
+  return x;
+}
 
 inline IpcExport ipc_export(const void *p) {
   IpcExport e;
@@ -341,8 +346,8 @@ inline IpcExport ipc_export(const void *p) {
   e.base = (uint64_t)(uintptr_t)base;
   e.offset = (uint64_t)((const char *)p - (const char *)base);
   if (ipc_debug())
-    ipc_note("[ipc %d] export %p = base %p + %llu (size %zu)\n", myid, p, (void *)base, (unsigned long long)e.offset,
-             size);
+    ipc_note("[ipc %d] export %p = base %p + %llu (size %zu) handle %016llx\n", myid, p, (void *)base,
+             (unsigned long long)e.offset, size, handle_hash(e.handle));
   return e;
 }
 
@@ -355,82 +360,31 @@ inline char *ipc_import(int peer, const IpcExport &e, std::vector<IpcKey> &held)
   if (it == m.end()) {
     void *ptr = nullptr;
     hip_check(hipIpcOpenMemHandle(&ptr, e.handle, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-    hipDeviceptr_t mb = nullptr;
-    size_t ms = 0;
-    if (hipMemGetAddressRange(&mb, &ms, (hipDeviceptr_t)ptr) != hipSuccess) {
-      (void)hipGetLastError();
-      ms = 0;
-    }
-    it = m.emplace(k, IpcMapping{(char *)ptr, 0, ms}).first;
+    it = m.emplace(k, IpcMapping{(char *)ptr, 0}).first;
   }
   it->second.refs++;
   held.push_back(k);
   if (ipc_debug())
-    ipc_note("[ipc %d] import peer %d base %#llx + %llu -> %p (refs %d)\n", myid, peer,
-                (unsigned long long)e.base, (unsigned long long)e.offset, (void *)(it->second.ptr + e.offset),
-                it->second.refs);
+    ipc_note("[ipc %d] import peer %d base %#llx + %llu -> %p (refs %d) handle %016llx\n", myid, peer,
+             (unsigned long long)e.base, (unsigned long long)e.offset, (void *)(it->second.ptr + e.offset),
+             it->second.refs, handle_hash(e.handle));
   return it->second.ptr + e.offset;
-}
-
-// HICCL_IPC_CLOSE (diagnostic): "now" (default) closes a mapping with its
-// last holder; "defer" keeps it open until ipc_close_retired() (after the
-// next communicator's imports, so those cannot land on its address);
-// "flush" also allocates and frees a scratch buffer after closing;
-// "reserve" closes and then reserves the freed address range (never mapped
-// again in this process).
-inline int ipc_close_mode() {
-  static const int m = [] {
-    const char *e = std::getenv("HICCL_IPC_CLOSE");
-    const std::string v = e ? e : "";
-    return v == "defer" ? 1 : v == "flush" ? 2 : v == "reserve" ? 3 : 0;
-  }();
-  return m;
-}
-inline std::vector<char *> &ipc_retired() {
-  static std::vector<char *> r;
-  return r;
-}
-inline void ipc_close_retired() {
-  for (char *p : ipc_retired()) {
-    if (ipc_debug()) ipc_note("[ipc %d] close retired %p\n", myid, (void *)p);
-    (void)hipIpcCloseMemHandle(p);
-  }
-  ipc_retired().clear();
 }
 
 inline void ipc_release(std::vector<IpcKey> &held) {
   auto &m = ipc_opened();
-  bool closed = false;
   for (const IpcKey &k : held) {
     auto it = m.find(k);
     if (it == m.end()) continue;
     if (--it->second.refs == 0) {
       if (ipc_debug())
-        ipc_note("[ipc %d] %s peer %d base %#llx at %p\n", myid, ipc_close_mode() == 1 ? "retire" : "close", k.rank,
-                 (unsigned long long)k.base, (void *)it->second.ptr);
-      if (ipc_close_mode() == 1) {
-        ipc_retired().push_back(it->second.ptr);
-      } else {
-        (void)hipIpcCloseMemHandle(it->second.ptr);
-        if (ipc_close_mode() == 3 && it->second.size) {
-          void *r = nullptr;
-          const hipError_t re = hipMemAddressReserve(&r, it->second.size, 0, it->second.ptr, 0);
-          if (re != hipSuccess) (void)hipGetLastError();
-          if (ipc_debug())
-            ipc_note("[ipc %d] reserve %p + %zu: %s at %p\n", myid, (void *)it->second.ptr, it->second.size,
-                     re == hipSuccess ? "ok" : "failed", r);
-          if (re == hipSuccess && r != it->second.ptr) (void)hipMemAddressFree(r, it->second.size);
-        }
-      }
-      closed = true;
+        ipc_note("[ipc %d] close peer %d base %#llx at %p\n", myid, k.rank, (unsigned long long)k.base,
+                 (void *)it->second.ptr);
+      (void)hipIpcCloseMemHandle(it->second.ptr);
       m.erase(it);
     }
   }
   held.clear();
-  if (closed && ipc_close_mode() == 2) {
-    void *scratch = nullptr;
-    if (hipMalloc(&scratch, (size_t)4 << 20) == hipSuccess) (void)hipFree(scratch);
-  }
 }
 
 // A communicator's flag array: one uint32 per slot in device memory on every

@@ -1,15 +1,14 @@
 // tests/cpp/ipc_reuse.cpp -- HIP IPC across buffer reuse (2 ranks, any GPUs).
 //
-// Each round rank 0 allocates a buffer of the same size (the allocator hands
-// back the freed address), fills it with the round number and exports it;
-// rank 1 opens the handle, reads it with a KERNEL (hiccl_stream_copy into a
-// local buffer) and writes a pattern into it with a kernel; rank 0 checks the
-// pattern landed, then frees.  Rank 1 closes the previous round's mapping
-// only right before it opens the next one, i.e. AFTER rank 0 allocated the
-// next buffer -- so that buffer gets new physical memory at the old virtual
-// address, and rank 1 typically maps it at its old virtual address too: a
-// stale translation or cache line on either side shows up as wrong bytes.
-//   mpirun -np 2 build/ipc_reuse [rounds] [bytes]
+// The pattern of a re-created communicator (tests/test_mpi_gpu.py
+// test_readme_api_example): every round rank 0 allocates two buffers S and R
+// (the allocator hands the freed addresses back, swapped), exports R
+// `exports` times (one hipIpcGetMemHandle per transfer into it), rank 1 opens
+// the first handle, writes the second half of R through it with a kernel
+// (hiccl_stream_copy), rank 0 writes the first half itself with a kernel and
+// checks both halves; then rank 1 closes its mapping, a barrier, and rank 0
+// frees S and R.  Prints whether the handle bytes repeat across rounds.
+//   mpirun -np 2 build/ipc_reuse [rounds] [bytes] [exports]
 #include <hip/hip_runtime.h>
 #include <mpi.h>
 
@@ -29,10 +28,10 @@
     }                                                                                                \
   } while (0)
 
-static size_t count_not(const std::vector<unsigned char> &h, unsigned char v) {
-  size_t n = 0;
-  for (unsigned char c : h) n += c != v;
-  return n;
+static size_t count_not(const unsigned char *h, size_t n, unsigned char v) {
+  size_t k = 0;
+  for (size_t i = 0; i < n; i++) k += h[i] != v;
+  return k;
 }
 
 int main(int argc, char **argv) {
@@ -40,7 +39,9 @@ int main(int argc, char **argv) {
   int me = 0;
   MPI_Comm_rank(MPI_COMM_WORLD, &me);
   const int rounds = argc > 1 ? std::atoi(argv[1]) : 6;
-  const size_t bytes = argc > 2 ? (size_t)std::atoll(argv[2]) : (size_t)1 << 22;
+  const size_t bytes = argc > 2 ? (size_t)std::atoll(argv[2]) : (size_t)2000000;
+  const int exports = argc > 3 ? std::atoi(argv[3]) : 4;
+  const size_t half = bytes / 2;
   int ndev = 0;
   CHECK(hipGetDeviceCount(&ndev));
   CHECK(hipSetDevice(me % ndev));
@@ -49,52 +50,45 @@ int main(int argc, char **argv) {
   void *local = nullptr;
   CHECK(hipMalloc(&local, bytes));
   std::vector<unsigned char> h(bytes);
+  std::vector<unsigned char> prev(sizeof(hipIpcMemHandle_t), 0);
   int bad = 0;
-  void *q = nullptr;  // rank 1: the current mapping
+  const int peer = 1 - me;
   for (int r = 0; r < rounds; r++) {
-    struct {
-      hipIpcMemHandle_t h;
-      unsigned long long va;
-    } msg;
-    void *p = nullptr;
-    const unsigned char mine = (unsigned char)(r + 1), theirs = (unsigned char)(101 + r);
-    if (me == 0) {
-      CHECK(hipMalloc(&p, bytes));
-      CHECK(hipMemset(p, mine, bytes));
-      CHECK(hipDeviceSynchronize());
-      CHECK(hipIpcGetMemHandle(&msg.h, p));
-      msg.va = (unsigned long long)(uintptr_t)p;
-      MPI_Send(&msg, sizeof(msg), MPI_BYTE, 1, r, MPI_COMM_WORLD);
-    } else if (me == 1) {
-      MPI_Recv(&msg, sizeof(msg), MPI_BYTE, 0, r, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
-      if (q) CHECK(hipIpcCloseMemHandle(q));  // the previous round's, only now
-      CHECK(hipIpcOpenMemHandle(&q, msg.h, hipIpcMemLazyEnablePeerAccess));
-      // kernel read through the mapping
-      if (hiccl_stream_copy(local, q, bytes, s)) MPI_Abort(MPI_COMM_WORLD, 2);
-      CHECK(hipStreamSynchronize(s));
-      CHECK(hipMemcpy(h.data(), local, bytes, hipMemcpyDeviceToHost));
-      const size_t rd = count_not(h, mine);
-      // kernel write through the mapping
-      CHECK(hipMemset(local, theirs, bytes));
-      CHECK(hipDeviceSynchronize());
-      if (hiccl_stream_copy(q, local, bytes, s)) MPI_Abort(MPI_COMM_WORLD, 2);
-      CHECK(hipStreamSynchronize(s));
-      std::printf("round %d: exporter va %#llx, mapped at %p, kernel read %zu wrong bytes\n", r, msg.va, q, rd);
-      bad += rd != 0;
-    }
+    // both ranks: S and R, R exported `exports` times; rank k owns half k of
+    // every R, writes it in its own R with its own kernel and in the peer's R
+    // through the peer's mapping
+    const unsigned char val[2] = {(unsigned char)(r + 1), (unsigned char)(101 + r)};
+    void *S = nullptr, *R = nullptr, *q = nullptr;
+    std::vector<hipIpcMemHandle_t> hs(exports), peer_hs(exports);
+    CHECK(hipMalloc(&S, bytes));
+    CHECK(hipMalloc(&R, bytes));
+    for (int k = 0; k < exports; k++) CHECK(hipIpcGetMemHandle(&hs[k], R));
+    MPI_Sendrecv(hs.data(), (int)(exports * sizeof(hipIpcMemHandle_t)), MPI_BYTE, peer, r, peer_hs.data(),
+                 (int)(exports * sizeof(hipIpcMemHandle_t)), MPI_BYTE, peer, r, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+    const bool same = std::memcmp(prev.data(), &hs[0], sizeof(hs[0])) == 0;
+    std::memcpy(prev.data(), &hs[0], sizeof(hs[0]));
+    CHECK(hipIpcOpenMemHandle(&q, peer_hs[0], hipIpcMemLazyEnablePeerAccess));
+    char *mine_half = (char *)R + (me ? half : 0);
+    char *theirs_half = (char *)q + (me ? half : 0);
+    const size_t n_mine = me ? bytes - half : half;
+    CHECK(hipMemset(local, val[me], bytes));
+    CHECK(hipDeviceSynchronize());
+    if (hiccl_stream_copy(mine_half, local, n_mine, s)) MPI_Abort(MPI_COMM_WORLD, 2);
+    if (hiccl_stream_copy(theirs_half, local, n_mine, s)) MPI_Abort(MPI_COMM_WORLD, 2);
+    CHECK(hipStreamSynchronize(s));
     MPI_Barrier(MPI_COMM_WORLD);
-    if (me == 0) {
-      CHECK(hipMemcpy(h.data(), p, bytes, hipMemcpyDeviceToHost));
-      const size_t wr = count_not(h, theirs);
-      std::printf("round %d: peer kernel write %zu wrong bytes\n", r, wr);
-      bad += wr != 0;
-      CHECK(hipFree(p));
-    }
+    CHECK(hipMemcpy(h.data(), R, bytes, hipMemcpyDeviceToHost));
+    const size_t w0 = count_not(h.data(), half, val[0]), w1 = count_not(h.data() + half, bytes - half, val[1]);
+    std::printf("round %d rank %d: S %p R %p mapped %p, handle %s, half0 %zu wrong, half1 %zu wrong\n", r, me, S, R, q,
+                same ? "REPEATED" : "new", w0, w1);
+    bad += (w0 || w1);
+    CHECK(hipIpcCloseMemHandle(q));
     MPI_Barrier(MPI_COMM_WORLD);
+    CHECK(hipFree(S));
+    CHECK(hipFree(R));
   }
-  if (q) CHECK(hipIpcCloseMemHandle(q));
   MPI_Allreduce(MPI_IN_PLACE, &bad, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
-  if (me == 0) std::printf("ipc_reuse: %s (%d bad checks over %d rounds)\n", bad ? "FAILED" : "PASSED", bad, rounds);
+  if (me == 0) std::printf("ipc_reuse: %s (%d bad rounds of %d)\n", bad ? "FAILED" : "PASSED", bad, rounds);
   MPI_Finalize();
   return bad ? 1 : 0;
 }
