@@ -26,7 +26,7 @@ int main(int argc, char **argv) {
   // previous round's are freed: a peer's new buffer may get the same address)
   const int rounds = argc > 3 ? std::atoi(argv[3]) : 1;
   unsigned long failed = 0;
-  // HICCL_README_KEEP_BUFFERS (diagnostic): one pair of user buffers for all rounds
+  // HICCL_README_KEEP_BUFFERS: one pair of user buffers for all rounds
   const bool keep = std::getenv("HICCL_README_KEEP_BUFFERS") != nullptr;
   T *sendbuf = nullptr;
   T *recvbuf = nullptr;
@@ -35,13 +35,9 @@ int main(int argc, char **argv) {
       allocate(sendbuf, count * numproc);
       allocate(recvbuf, count * numproc);
     }
-    if (std::getenv("HICCL_README_TOUCH")) {  // diagnostic: this rank writes its recvbuf once before any peer
-      std::vector<T> zero(count * numproc, (T)0);
-      CommBench::memcpyH2D(recvbuf, zero.data(), zero.size());
-    }
 
-    // the communicator goes before its buffers: a peer must close its IPC mapping
-    // of a buffer before the owner frees it (hipIpcOpenMemHandle: UB otherwise)
+    // the communicator goes before its buffers (its teardown is collective:
+    // every peer releases its mappings of them first)
     {
       Comm<T> allreduce;
 
@@ -75,17 +71,7 @@ int main(int argc, char **argv) {
       }
 
       std::vector<T> out(count * numproc);
-#ifndef HICCL_PORT_HOST
-      if (std::getenv("HICCL_README_KERNEL_READ")) {  // diagnostic: read back through a kernel copy
-        T *tmp = nullptr;
-        allocate(tmp, out.size());
-        if (hiccl_stream_copy(tmp, recvbuf, out.size() * sizeof(T), nullptr)) CommBench::die("copy", "");
-        CommBench::hip_check(hipDeviceSynchronize(), "sync");
-        CommBench::memcpyD2H(out.data(), tmp, out.size());
-        free(tmp);
-      } else
-#endif
-        CommBench::memcpyD2H(out.data(), recvbuf, out.size());
+      CommBench::memcpyD2H(out.data(), recvbuf, out.size());
       const double ranks = (double)numproc * (numproc + 1) / 2 + (double)round * numproc;
       size_t errors = 0;
       for (size_t i = 0; i < out.size(); i++)
@@ -103,7 +89,7 @@ int main(int argc, char **argv) {
       if (total) CommBench::ipc_log_dump();  // HICCL_DEBUG_IPC=2
 #endif
     }
-    if ((!keep || round == rounds - 1) && !std::getenv("HICCL_README_NOFREE")) {  // NOFREE: diagnostic leak
+    if (!keep || round == rounds - 1) {
       free(sendbuf);
       free(recvbuf);
     }

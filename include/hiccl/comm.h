@@ -512,13 +512,11 @@ class Comm {
 
  public:
   // The schedule's receive / partial buffers are freed with the communicator
-  // (the reference leaks them).  Collective: every rank first closes its IPC
-  // mappings of its peers' buffers (deleting the transports), then a barrier,
-  // then the buffers are freed -- HIP leaves freeing an exported allocation
-  // that another process still has open undefined (hipIpcOpenMemHandle), and
-  // on MI355X it loses writes made through the peer's next mapping of that
-  // address.  The same order is the caller's duty for its own buffers:
-  // destroy the communicator before freeing what it was built on.
+  // (the reference leaks them).  Collective: every rank first releases its
+  // IPC mappings of its peers' buffers (deleting the transports; the
+  // mappings are retired, see CommBench::IpcMapping), then a barrier, then
+  // the buffers are freed.  Destroy the communicator before freeing the
+  // buffers it was built on.
   ~Comm() {
     if (running) pthread_join(thread, nullptr);  // a start() without wait(): finish it first
 #ifndef HICCL_PORT_HOST
@@ -526,7 +524,7 @@ class Comm {
     if (graph_ctr) (void)hipFree(graph_ctr);
     if (!owned.empty() || !command_batch.empty()) (void)hipDeviceSynchronize();
 #endif
-    // the steps' transports (closing their IPC mappings) and computes (the
+    // the steps' transports (releasing their IPC mappings) and computes (the
     // reference never deletes them)
     for (auto &lst : command_batch)
       for (auto &c : lst) {
@@ -538,7 +536,7 @@ class Comm {
     flags.close();  // peers' flag arrays
     int fin = 0;
     MPI_Finalized(&fin);
-    if (!fin) MPI_Barrier(CommBench::comm_mpi);  // every peer's mappings of this rank's buffers are closed
+    if (!fin) MPI_Barrier(CommBench::comm_mpi);  // every peer has released its mappings of this rank's buffers
 #endif
     for (T *p : owned) CommBench::free(p);
   }

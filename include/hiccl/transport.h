@@ -289,20 +289,62 @@ struct IpcExport {
   hipIpcMemHandle_t handle;
   uint64_t base;    // peer's allocation base (identifies the mapping)
   uint64_t offset;  // byte offset of the buffer inside that allocation
+  uint64_t nonce;   // probe value written at the buffer (probe != 0), see ipc_probe_*
+  uint32_t probe;   // bytes of the probe (0: no probe)
+  uint32_t recycled;  // the base was exported before for another allocation
 };
 
-// Mappings are reference-counted per holder (a transport, a flag space) and
-// closed with the last holder: a peer that frees an allocation and gets the
-// same base address again for a new one (the next communicator's buffers)
-// must never be reached through the old mapping.
+// Mappings are reference-counted per holder (a transport, a flag space).
+// When the last holder lets go, the mapping is RETIRED, not closed: on ROCm
+// 7.2 (dmabuf IPC) closing a mapping and later opening a peer's NEW
+// allocation that the peer's allocator placed at a freed exported address
+// yields a mapping that reaches other memory -- writes through it are lost
+// (measured: 4 ranks x 5 recreated communicators on reallocated buffers fail
+// within 1-3 runs when mappings are closed, never when they stay open; a
+// 200 ms pause after the close does not help; tests/test_mpi_gpu.py
+// ::test_recreated_communicators_on_reallocated_buffers).  A retired
+// mapping is revived when the peer exports the same allocation again (same
+// base, not recycled) and closed, oldest first, only when the retired
+// mappings exceed HICCL_IPC_RETIRED_MAX bytes (default: a quarter of the
+// device's memory; they keep the peers' freed allocations alive) or on
+// ipc_trim().  A mapping opened for a recycled address is verified by a
+// probe (ipc_probe_*), so a closed-then-reopened address that misses fails
+// loudly instead of losing data.
 struct IpcMapping {
   char *ptr;
   int refs;
+  size_t bytes;  // of the mapped allocation
 };
 
 inline std::map<IpcKey, IpcMapping> &ipc_opened() {
   static std::map<IpcKey, IpcMapping> m;
   return m;
+}
+
+struct IpcRetired {
+  IpcKey key;
+  char *ptr;
+  size_t bytes;
+};
+inline std::vector<IpcRetired> &ipc_retired() {  // oldest first
+  static std::vector<IpcRetired> r;
+  return r;
+}
+inline size_t &ipc_retired_bytes() {
+  static size_t b = 0;
+  return b;
+}
+inline size_t ipc_retired_max() {
+  static const size_t cap = [] {
+    if (const char *e = std::getenv("HICCL_IPC_RETIRED_MAX")) return (size_t)std::strtoull(e, nullptr, 0);
+    size_t fr = 0, total = 0;
+    if (hipMemGetInfo(&fr, &total) != hipSuccess) {
+      (void)hipGetLastError();
+      return (size_t)16 << 30;
+    }
+    return total / 4;
+  }();
+  return cap;
 }
 
 // HICCL_DEBUG_IPC=1: every export, import and close on stdout; =2: kept in
@@ -329,6 +371,16 @@ inline void ipc_log_dump() {
   std::fputs(ipc_log().c_str(), stdout);
   std::fflush(stdout);
 }
+inline std::string handle_hex(const hipIpcMemHandle_t &h) {  // the handle's bytes as 32-bit words
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(&h);
+  std::string s;
+  char b[12];
+  for (size_t i = 0; i < sizeof(h) / 4; i++) {
+    std::snprintf(b, sizeof(b), "%s%x", i ? "." : "", w[i]);
+    s += b;
+  }
+  return s;
+}
 inline unsigned long long handle_hash(const hipIpcMemHandle_t &h) {  // FNV-1a of the handle bytes
   const unsigned char *b = reinterpret_cast<const unsigned char *>(&h);
   unsigned long long x = 1469598103934665603ull;
@@ -336,7 +388,18 @@ inline unsigned long long handle_hash(const hipIpcMemHandle_t &h) {  // FNV-1a o
   return x;
 }
 
-inline IpcExport ipc_export(const void *p) {
+// Allocation ids (HIP's unique buffer id per allocation) of the bases this
+// process has exported, per importing rank: a base exported again to that
+// rank for a DIFFERENT allocation is a recycled address (an exported buffer
+// was freed and the allocator handed its address back), which the importer
+// must neither revive its retired mapping for nor trust unverified.
+inline std::map<std::pair<uintptr_t, int>, unsigned long long> &ipc_exported_ids() {
+  static std::map<std::pair<uintptr_t, int>, unsigned long long> m;
+  return m;
+}
+
+// `to`: the importing rank, or -1 for every other rank (a flag space).
+inline IpcExport ipc_export(const void *p, int to) {
   IpcExport e;
   std::memset(&e, 0, sizeof(e));
   hipDeviceptr_t base = nullptr;
@@ -345,22 +408,107 @@ inline IpcExport ipc_export(const void *p) {
   hip_check(hipIpcGetMemHandle(&e.handle, (void *)base), "hipIpcGetMemHandle");
   e.base = (uint64_t)(uintptr_t)base;
   e.offset = (uint64_t)((const char *)p - (const char *)base);
+  unsigned long long id = 0;
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, base) != hipSuccess) {
+    (void)hipGetLastError();
+    e.recycled = 1;  // unknown: never revive, verify
+  } else {
+    auto &ids = ipc_exported_ids();
+    for (int r = 0; r < numproc; r++) {
+      if (r == myid || (to >= 0 && r != to)) continue;
+      auto it = ids.find({(uintptr_t)base, r});
+      if (it != ids.end() && it->second != id) e.recycled = 1;
+      ids[{(uintptr_t)base, r}] = id;
+    }
+  }
   if (ipc_debug())
-    ipc_note("[ipc %d] export %p = base %p + %llu (size %zu) handle %016llx\n", myid, p, (void *)base,
-             (unsigned long long)e.offset, size, handle_hash(e.handle));
+    ipc_note("[ipc %d] export %p = base %p + %llu (size %zu)%s handle %016llx [%s]\n", myid, p, (void *)base,
+             (unsigned long long)e.offset, size, e.recycled ? " recycled" : "", handle_hash(e.handle),
+             handle_hex(e.handle).c_str());
   return e;
+}
+
+// Probe of a mapping of a recycled base (owner side, before the export is
+// sent): save the first `bytes` (<= 8) of the buffer, write a nonce there.
+// The mover reads them through its mapping (ipc_probe_check) and answers;
+// ipc_probe_finish restores the bytes (see IpcMapping for why).
+inline uint64_t ipc_probe_begin(IpcExport &e, void *p, size_t bytes) {
+  static uint64_t counter = 0x9e3779b97f4a7c15ull;
+  uint64_t saved = 0;
+  e.probe = (uint32_t)std::min<size_t>(bytes, 8);
+  if (!e.probe) return 0;
+  hip_check(hipMemcpy(&saved, p, e.probe, hipMemcpyDeviceToHost), "probe save");
+  counter = counter * 6364136223846793005ull + 1442695040888963407ull + (uint64_t)myid;
+  e.nonce = counter ^ saved;  // never the current contents
+  if (std::memcmp(&e.nonce, &saved, e.probe) == 0) e.nonce = ~saved;
+  hip_check(hipMemcpy(p, &e.nonce, e.probe, hipMemcpyHostToDevice), "probe write");
+  return saved;
+}
+// 0: both views see the nonce; bit 0: the copy engine's view differs; bit 1:
+// a kernel's view (what the transfers use) differs.
+inline int ipc_probe_check(const IpcExport &e, const void *mapped, std::string *seen = nullptr) {
+  uint64_t got = 0, got_k = 0;
+  hip_check(hipMemcpy(&got, mapped, e.probe, hipMemcpyDeviceToHost), "probe read");
+  static uint64_t *scratch = nullptr;
+  if (!scratch) hip_check(hipMalloc((void **)&scratch, 64), "probe scratch");
+  if (hiccl_stream_copy(scratch, mapped, e.probe, nullptr)) die("probe", hiccl_last_error());
+  hip_check(hipDeviceSynchronize(), "probe sync");
+  hip_check(hipMemcpy(&got_k, scratch, e.probe, hipMemcpyDeviceToHost), "probe read (kernel)");
+  if (seen) {
+    char b[160];
+    std::snprintf(b, sizeof(b), "nonce %016llx, copy engine %016llx, kernel %016llx", (unsigned long long)e.nonce,
+                  (unsigned long long)got, (unsigned long long)got_k);
+    *seen = b;
+  }
+  return (std::memcmp(&got, &e.nonce, e.probe) != 0) | (std::memcmp(&got_k, &e.nonce, e.probe) != 0) << 1;
+}
+inline void ipc_probe_finish(const IpcExport &e, void *p, uint64_t saved) {
+  hip_check(hipMemcpy(p, &saved, e.probe, hipMemcpyHostToDevice), "probe restore");
 }
 
 // The mapping of peer's exported buffer; its key is appended to `held`,
 // which the holder hands to ipc_release when it no longer uses the mapping.
+inline void ipc_close_oldest_retired() {
+  auto &r = ipc_retired();
+  if (r.empty()) return;
+  if (ipc_debug())
+    ipc_note("[ipc %d] close retired peer %d base %#llx at %p\n", myid, r.front().key.rank,
+             (unsigned long long)r.front().key.base, (void *)r.front().ptr);
+  (void)hipIpcCloseMemHandle(r.front().ptr);
+  ipc_retired_bytes() -= r.front().bytes;
+  r.erase(r.begin());
+}
+
+// Close every retired mapping (the peers' freed allocations they keep alive
+// are released).  Safe whenever no communicator is being created.
+inline void ipc_trim() {
+  while (!ipc_retired().empty()) ipc_close_oldest_retired();
+}
+
 inline char *ipc_import(int peer, const IpcExport &e, std::vector<IpcKey> &held) {
   IpcKey k{peer, (uintptr_t)e.base};
   auto &m = ipc_opened();
   auto it = m.find(k);
   if (it == m.end()) {
-    void *ptr = nullptr;
-    hip_check(hipIpcOpenMemHandle(&ptr, e.handle, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-    it = m.emplace(k, IpcMapping{(char *)ptr, 0}).first;
+    auto &r = ipc_retired();
+    auto rit = r.end();
+    for (auto i = r.begin(); i != r.end(); ++i)  // the most recent retired mapping of this base
+      if (i->key.rank == k.rank && i->key.base == k.base) rit = i;
+    if (rit != r.end() && !e.recycled) {  // the same allocation as when it was retired: revive
+      it = m.emplace(k, IpcMapping{rit->ptr, 0, rit->bytes}).first;
+      ipc_retired_bytes() -= rit->bytes;
+      r.erase(rit);
+    } else {
+      void *ptr = nullptr;
+      hip_check(hipIpcOpenMemHandle(&ptr, e.handle, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+      hipDeviceptr_t mb = nullptr;
+      size_t bytes = 0;
+      if (hipMemGetAddressRange(&mb, &bytes, (hipDeviceptr_t)ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        bytes = 0;
+      }
+      it = m.emplace(k, IpcMapping{(char *)ptr, 0, bytes}).first;
+    }
   }
   it->second.refs++;
   held.push_back(k);
@@ -378,13 +526,15 @@ inline void ipc_release(std::vector<IpcKey> &held) {
     if (it == m.end()) continue;
     if (--it->second.refs == 0) {
       if (ipc_debug())
-        ipc_note("[ipc %d] close peer %d base %#llx at %p\n", myid, k.rank, (unsigned long long)k.base,
+        ipc_note("[ipc %d] retire peer %d base %#llx at %p\n", myid, k.rank, (unsigned long long)k.base,
                  (void *)it->second.ptr);
-      (void)hipIpcCloseMemHandle(it->second.ptr);
+      ipc_retired().push_back(IpcRetired{k, it->second.ptr, it->second.bytes});
+      ipc_retired_bytes() += it->second.bytes;
       m.erase(it);
     }
   }
   held.clear();
+  while (!ipc_retired().empty() && ipc_retired_bytes() > ipc_retired_max()) ipc_close_oldest_retired();
 }
 
 // A communicator's flag array: one uint32 per slot in device memory on every
@@ -411,7 +561,7 @@ struct FlagSpace {
     hip_check(hipHostMalloc((void **)&err, sizeof(uint32_t), hipHostMallocCoherent), "hipHostMalloc(err)");
     *err = 0;
     hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize(flags)");
-    IpcExport mine = ipc_export(local);
+    IpcExport mine = ipc_export(local, -1);
     std::vector<IpcExport> all(numproc);
     mpi_check(MPI_Allgather(&mine, sizeof(IpcExport), MPI_BYTE, all.data(), sizeof(IpcExport), MPI_BYTE, comm_mpi),
               "MPI_Allgather(flags)");
@@ -576,8 +726,19 @@ class Comm {
       // the mover needs a mapping of the owner's buffer
       const int owner = owner_of(x), mover = mover_of(x);
       if (myid == owner) {
-        IpcExport e = ipc_export(owner == x.sendid ? x.src : x.dst);
+        T *mine = owner == x.sendid ? x.src : x.dst;
+        IpcExport e = ipc_export(mine, mover);
+        const uint64_t saved = e.recycled ? ipc_probe_begin(e, mine, count * sizeof(T)) : 0;
         mpi_check(MPI_Send(&e, sizeof(e), MPI_BYTE, mover, x.tag, comm_mpi), "MPI_Send(ipc)");
+        if (e.probe) {
+          int ok = 0;
+          mpi_check(MPI_Recv(&ok, 1, MPI_INT, mover, x.tag, comm_mpi, MPI_STATUS_IGNORE), "MPI_Recv(probe)");
+          ipc_probe_finish(e, mine, saved);
+          if (!ok)
+            die("transport", "rank " + std::to_string(mover) + "'s IPC mapping of a reallocated buffer of this rank "
+                "does not reach it (the runtime reused a freed exported allocation's address); keep buffers "
+                "registered with a communicator allocated until the last communicator using them is destroyed");
+        }
       }
       if (myid == mover) {
         IpcExport e;
@@ -588,6 +749,16 @@ class Comm {
         MPI_Get_count(&st, MPI_BYTE, &got);
         if (got != (int)sizeof(e)) die("transport", "IPC handle exchange matched a message of " + std::to_string(got) + " bytes");
         x.remote = ipc_import(owner, e, held);
+        if (e.probe) {
+          std::string seen;
+          int bad = ipc_probe_check(e, x.remote, &seen);
+          int ok = bad == 0;
+          if (ipc_debug()) ipc_note("[ipc %d] probe peer %d base %#llx: %d\n", myid, owner,
+                                    (unsigned long long)e.base, bad);
+          mpi_check(MPI_Send(&ok, 1, MPI_INT, owner, x.tag, comm_mpi), "MPI_Send(probe)");
+          if (!ok) die("transport", "this rank's IPC mapping of a reallocated buffer of rank " + std::to_string(owner) +
+                                    " does not reach it (" + seen + ")");
+        }
       }
     }
     if (sendid != recvid && lib == MPI && (myid == sendid || myid == recvid))

@@ -131,24 +131,45 @@ def test_known_answer_graph_replay(np_, hier, libs, pattern):
 
 @pytest.mark.parametrize("streamed", [True, False], ids=["stream", "host"])
 @pytest.mark.parametrize("np_", [2, 4])
-def test_readme_api_example(np_, streamed):
+@pytest.mark.parametrize("count", [250000, 1 << 22])
+def test_readme_api_example(np_, streamed, count):
     """Three rounds on the same user buffers, each with a fresh communicator
-    (its schedule buffers freed and reallocated, every IPC mapping closed
-    and opened again: the schedule's buffers come back at the freed
-    addresses, which must not be reached through a stale mapping)."""
-    rc, out = mpirun(np_, os.path.join(ROOT, "build", "readme_example_hip"), [250000, 3, 3], streamed=streamed,
+    (its schedule buffers freed and reallocated -- sub-allocated at 1 MB,
+    dedicated allocations at 16 MiB -- and every IPC mapping released: the
+    user buffers' mappings are revived, the schedule buffers' come back at
+    recycled addresses and are opened anew)."""
+    rc, out = mpirun(np_, os.path.join(ROOT, "build", "readme_example_hip"), [count, 3, 3], streamed=streamed,
                      extra_env={"HICCL_README_KEEP_BUFFERS": "1"})
     assert rc == 0, out[-3000:]
     assert out.count("README all-reduce: PASSED") == 3, out[-3000:]
 
 
-@pytest.mark.xfail(strict=False, reason="open (DESIGN.md section 6): with the USER's buffers freed and "
-                   "reallocated between communicators, a peer's writes into the new buffer are lost in some "
-                   "rounds; mappings and pointers verified correct (HICCL_DEBUG_IPC=2), the same pattern in "
-                   "tests/cpp/ipc_reuse.cpp does not reproduce it")
-def test_readme_recreated_with_reallocated_user_buffers():
-    rc, out = mpirun(2, os.path.join(ROOT, "build", "readme_example_hip"), [250000, 3, 4], streamed=False)
-    assert rc == 0 and out.count("README all-reduce: PASSED") == 4, out[-3000:]
+@pytest.mark.parametrize("streamed", [True, False], ids=["stream", "host"])
+@pytest.mark.parametrize("np_", [2, 4])
+def test_recreated_communicators_on_reallocated_buffers(np_, streamed):
+    """Five rounds, each with fresh user buffers (the previous round's freed:
+    the allocator hands exported addresses back for new allocations) and a
+    fresh communicator.  Closing a peer's mapping and opening its new
+    allocation at the recycled address reaches other memory on ROCm 7.2
+    (DESIGN.md section 6); the transport retires mappings instead, and every
+    round must pass."""
+    rc, out = mpirun(np_, os.path.join(ROOT, "build", "readme_example_hip"), [250000, 3, 5], streamed=streamed)
+    assert rc == 0, out[-3000:]
+    assert out.count("README all-reduce: PASSED") == 5, out[-3000:]
+
+
+def test_recycled_address_never_silently_wrong():
+    """With retirement off (HICCL_IPC_RETIRED_MAX=0: every released mapping is
+    closed at once) a mapping of a recycled address may miss; the probe at
+    init must then stop the job with its error -- a round that completes is
+    correct, a FAILED round is never printed."""
+    for _ in range(3):
+        rc, out = mpirun(4, os.path.join(ROOT, "build", "readme_example_hip"), [250000, 3, 5], streamed=False,
+                         extra_env={"HICCL_IPC_RETIRED_MAX": "0"})
+        assert "FAILED" not in out, out[-3000:]
+        if rc != 0:
+            assert "does not reach it" in out, out[-3000:]
+            return
 
 
 @pytest.mark.parametrize("pattern", [8, 7])
