@@ -287,6 +287,20 @@ def mix_ceiling(ins, out, count, reps=10, mode=0):
     return best
 
 
+def serial_rw_model(read_bytes, write_bytes, read_gbps, copy_gbps, kern_s):
+    """The box's own HBM bound for a read/write mix: a DRAM channel either
+    reads or writes, so a kernel that reads R and writes W bytes needs at
+    least R / read_rate + W / write_rate.  read_rate = the 8-stream read-only
+    probe on the bench's buckets; write_rate from the copy probe (X read + X
+    written in t: X / t_write = X / (t - X / read_rate))."""
+    if not read_gbps or not copy_gbps or 2.0 / copy_gbps <= 1.0 / read_gbps:
+        return None
+    write_gbps = 1.0 / (2.0 / copy_gbps - 1.0 / read_gbps)
+    t = read_bytes / read_gbps / 1e9 + write_bytes / write_gbps / 1e9
+    return {"read_GBps": round(read_gbps, 1), "write_GBps_from_copy": round(write_gbps, 1),
+            "predicted_ms": round(t * 1e3, 4), "frac": round(t / kern_s, 4)}
+
+
 def copy_ceiling(nbytes=1 << 30, reps=10):
     src = torch.empty(nbytes // 4, device="cuda")
     dst = torch.empty_like(src)
@@ -596,6 +610,7 @@ def main():
     # HBM3E moves 4 bits per pin per reported memory clock (8 Gb/s per pin at
     # the 2 GHz the runtime reports on MI355X): 8192 bits -> 8.19 TB/s, the spec
     props_peak = 4.0 * mclk.value * 1e3 * bus.value / 8 / 1e9
+    serial = serial_rw_model(n * count * 4, count * 4, read_gbps, copy_gbps, kern_s)
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -626,6 +641,7 @@ def main():
                      "frac_of_read_ceiling": round(achieved / read_gbps, 4) if read_gbps else None,
                      "copy_ceiling_GBps": round(copy_gbps, 1) if copy_gbps else None,
                      "frac_of_copy": round(achieved / copy_gbps, 4) if copy_gbps else None,
+                     "serial_rw_model": serial,
                      "traffic_source": (prof or {}).get("source")},
         "cpu_baseline": cpu,
         "parity_full": parity_full,
