@@ -121,3 +121,19 @@ def test_cpu_leg_full_bucket_parity(tmp_path):
         r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
         assert r["parity_full"]["ok"] is ok and r["parity_full"]["mismatches"] == mism
         assert r["threads"] == 2 and "OMP_PROC_BIND=spread" in r["sample"]
+
+
+def test_serial_rw_model():
+    """roofline.serial_rw_model: R / read_rate + W / write_rate, the write
+    rate recovered from the copy probe (X read + X written)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    read, write = 7000.0, 4500.0
+    copy = 2.0 / (1.0 / read + 1.0 / write)  # what a copy probe would measure
+    r, w = 8 * 2**30, 2**30
+    t = r / read / 1e9 + w / write / 1e9
+    m = bench.serial_rw_model(r, w, read, copy, t)
+    assert abs(m["write_GBps_from_copy"] - write) < 0.1
+    assert abs(m["predicted_ms"] - t * 1e3) < 1e-3 and abs(m["frac"] - 1.0) < 1e-3
+    assert bench.serial_rw_model(r, w, None, copy, t) is None
+    assert bench.serial_rw_model(r, w, read, 2 * read, t) is None  # copy faster than reads: no model
