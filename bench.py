@@ -159,6 +159,9 @@ def run_c5(world, args, allow_shared=False):
     modes = [("host", {"HICCL_STREAM_ORDERED": "0"}, hier, libs),
              ("stream_graph", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "0"}, hier, libs),
              ("stream_graph_fused", fused, hier, libs)]
+    # the reference's main.cu runs its levels on XCCL (main.cu:25): RCCL
+    # point-to-point per level (on shared GPUs the library falls back to IPC)
+    modes.append(("xccl", {"HICCL_STREAM_ORDERED": "0"}, hier, libs.replace("ipc", "xccl")))
     if hier != str(world):
         # not the reference's config: the same all-reduce on one flat IPC
         # level, every peer over its own xGMI link of the full mesh ({1,4,2}

@@ -17,12 +17,13 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("ranks", [2, 4])
 def test_c5_leg_rehearsal_one_gpu(ranks):
-    """4 ranks: hierarchy {1,2,2} {MPI,IPC,IPC} plus the flat {4} {IPC} run."""
+    """4 ranks: hierarchy {1,2,2} {MPI,IPC,IPC}, the same on XCCL levels (RCCL
+    refuses shared GPUs: the IPC fallback here), plus the flat {4} {IPC} run."""
     import bench
     res = bench.run_c5(ranks, argparse.Namespace(c5_log2count=14, c5_iters=2), allow_shared=True)
     assert "workload" in res, res
-    modes = ["host", "stream_graph", "stream_graph_fused"] + (["flat_stream_graph_fused"] if ranks > 2 else [])
-    assert [m for m in res if m.endswith(("host", "fused", "graph"))] == modes
+    modes = ["host", "stream_graph", "stream_graph_fused", "xccl"] + (["flat_stream_graph_fused"] if ranks > 2 else [])
+    assert [m for m in res if m.endswith(("host", "fused", "graph", "xccl"))] == modes
     for mode in modes:
         r = res[mode]
         assert r.get("kat") == "PASSED", r
