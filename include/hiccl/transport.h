@@ -120,6 +120,14 @@ inline void init() {
   if (ndev < 1) die("init", "no HIP device");
   mydevice = lrank % ndev;
   setup_gpu();
+  // HICCL_SYNC=spin|yield|blocking: how host synchronisations wait (HIP's
+  // default is auto); host-driven steps synchronise twice per step
+  if (const char *m = std::getenv("HICCL_SYNC")) {
+    const std::string v = m;
+    const unsigned f = v == "spin" ? hipDeviceScheduleSpin : v == "yield" ? hipDeviceScheduleYield
+                       : v == "blocking" ? hipDeviceScheduleBlockingSync : hipDeviceScheduleAuto;
+    if (hipSetDeviceFlags(f) != hipSuccess) (void)hipGetLastError();
+  }
 #endif
 }
 
