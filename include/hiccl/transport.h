@@ -474,8 +474,6 @@ inline void ipc_probe_finish(const IpcExport &e, void *p, uint64_t saved) {
   hip_check(hipMemcpy(p, &saved, e.probe, hipMemcpyHostToDevice), "probe restore");
 }
 
-// The mapping of peer's exported buffer; its key is appended to `held`,
-// which the holder hands to ipc_release when it no longer uses the mapping.
 inline void ipc_close_oldest_retired() {
   auto &r = ipc_retired();
   if (r.empty()) return;
@@ -493,6 +491,8 @@ inline void ipc_trim() {
   while (!ipc_retired().empty()) ipc_close_oldest_retired();
 }
 
+// The mapping of peer's exported buffer; its key is appended to `held`,
+// which the holder hands to ipc_release when it no longer uses the mapping.
 inline char *ipc_import(int peer, const IpcExport &e, std::vector<IpcKey> &held) {
   IpcKey k{peer, (uintptr_t)e.base};
   auto &m = ipc_opened();
@@ -744,8 +744,8 @@ class Comm {
           ipc_probe_finish(e, mine, saved);
           if (!ok)
             die("transport", "rank " + std::to_string(mover) + "'s IPC mapping of a reallocated buffer of this rank "
-                "does not reach it (the runtime reused a freed exported allocation's address); keep buffers "
-                "registered with a communicator allocated until the last communicator using them is destroyed");
+                "does not reach it (the peer closed an earlier mapping of this freed and reused address: raise "
+                "HICCL_IPC_RETIRED_MAX, or keep the buffers allocated across communicators)");
         }
       }
       if (myid == mover) {
