@@ -848,3 +848,20 @@ def test_dynamic_schedule_per_thread_stream_two_threads(oracle):
     for (ins, out), e in zip(bufs, exps):
         got = out.cpu().numpy()
         assert bits_equal(got, e), first_mismatch(got, e)
+
+
+@pytest.mark.parametrize("offs,out_off", [([1, 0], 0), ([0, 3], 1), ([1, 2, 3, 0], 0), ([3, 3, 3], 3),
+                                          ([2, 1, 0, 3, 2, 1, 0, 3, 1], 0), ([1, 2, 3, 1, 2, 3, 1, 2], 0),
+                                          ([1, 2, 3, 1, 2, 3, 1, 2], 1)])
+@pytest.mark.parametrize("dtype", [np.float32, np.uint16])
+def test_misaligned_full_tiles(oracle, offs, out_off, dtype):
+    """Inputs off a 16-B boundary on the full 256 x 4 tile shape (the C2
+    shape; the small-count tests above run on half tiles): bit-exact
+    against the oracle across tile boundaries and partial last tiles."""
+    n = len(offs)
+    cfg = dict(engine=hiccl_amd.HICCL_ENGINE_TILE, block=256, unroll=4)
+    for count in (1, 5, 4099, 70001, (1 << 20) + 3, 3 * 4096 * 64 + 7):
+        x = oracle.fill(n, count, seed=17 + count, dtype=dtype)
+        got = gpu_reduce(x, count, dtype, offsets=offs, out_offset=out_off, config=cfg)
+        exp = oracle.reduce(list(x), dtype=dtype)
+        assert bits_equal(got, exp), f"offs={offs} out={out_off} count={count}: {first_mismatch(got, exp)}"
