@@ -889,7 +889,9 @@ def c2variants(args):
     n = 8
     cases = [("readme_count", 250_000_000, [0] * n, 0),
              ("inputs_shifted", 1 << 28, [1 + k % 3 for k in range(n)], 0),
-             ("inputs_and_output_shifted", 1 << 28, [1 + k % 3 for k in range(n)], 1)]
+             ("inputs_and_output_shifted", 1 << 28, [1 + k % 3 for k in range(n)], 1),
+             ("inputs_common_shift", 1 << 28, [1] * n, 0),
+             ("output_shifted", 1 << 28, [0] * n, 1)]
     for name, count, in_off, out_off in cases:
         bases = [torch.empty(count + 4, dtype=torch.float32, device="cuda") for _ in range(n)]
         ins = [b[o:o + count] for b, o in zip(bases, in_off)]
@@ -898,6 +900,7 @@ def c2variants(args):
         obase = torch.empty(count + 4, dtype=torch.float32, device="cuda")
         out = obase[out_off:out_off + count]
         torch.cuda.synchronize()
+        out.fill_(float("nan"))
         _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins), args.steps, args.warmup)
         t = float(np.median(ms)) * 1e-3
         b = (n + 1) * count * 4
