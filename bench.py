@@ -518,6 +518,8 @@ def main():
     ap.add_argument("--buckets", type=int, default=0, help="schedsweep: this many fresh --n x 2^--log2count buckets")
     ap.add_argument("--cpu-leg", action="store_true", help=argparse.SUPPRESS)  # child of cpu_baseline()
     ap.add_argument("--expect-file", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--no-misaligned", action="store_true",
+                    help="skip the misaligned second C2 run (rocprofv3 runs: one kernel shape per trace)")
     ap.add_argument("--no-c5", action="store_true", help="N > 1: skip the config-5 all-reduce leg")
     ap.add_argument("--c5-log2count", type=int, default=25,
                     help="config-5 leg: elements per rank per chunk = 2^x (25: 1 GiB fp32 send buffer at 8 ranks)")
@@ -596,6 +598,7 @@ def main():
 
     parity = bool(dist.max(0.0 if parity in (True, None) else 1.0) == 0.0) if parity is not None else None
     copy_gbps = copy_ceiling() if dist.rank == 0 else None
+    misaligned = c2_misaligned(n, count, args.steps, args.warmup) if dist.rank == 0 and cfg is None and not args.no_misaligned else None
     prof = traffic_from_profiles(n, count) if cfg is None else None
     cpu, parity_full = None, None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
@@ -638,6 +641,7 @@ def main():
                      "read_frac": round(n * count * 4 / kern_s / 1e9 / HBM_PEAK_GBPS, 4),
                      "traffic": (prof or {}).get("hbm_bytes_per_launch"),
                      "kernel_ms_mean": round(kern_s * 1e3, 4), "kernel_ms_min": round(min(kms), 4),
+                     "kernel_ms_median": round(float(np.median(kms)), 4), "kernel_ms_max": round(max(kms), 4),
                      "mix_ceiling_GBps": round(mix_gbps, 1) if mix_gbps else None,
                      "frac_of_mix_ceiling": round(achieved / mix_gbps, 4) if mix_gbps else None,
                      "read_ceiling_GBps": round(read_gbps, 1) if read_gbps else None,
@@ -655,6 +659,8 @@ def main():
                          "total_mem_GiB": round(props.total_memory / 2**30, 1)},
         "control_plane": dist.backend,
     }
+    if misaligned is not None:
+        line["c2_misaligned"] = misaligned
     if c5 is not None:
         line["c5"] = c5
     print(json.dumps(line), flush=True)
@@ -879,6 +885,29 @@ def crossover(args):
                 del ins, out
                 torch.cuda.empty_cache()
     return 0
+
+
+def c2_misaligned(n, count, steps, warmup):
+    """SURVEY.md 8d's second C2 run: the same bucket with input k placed
+    1 + k mod 3 elements past a 16-B boundary (the mutual misalignment
+    partition() produces, reduce.h:401-415), output aligned; fresh buffers,
+    the headline's steps/warmup, a sampled bitwise check."""
+    offs = [1 + k % 3 for k in range(n)]
+    bases = [torch.empty(count + 4, dtype=torch.float32, device="cuda") for _ in range(n)]
+    ins = [b[o:o + count] for b, o in zip(bases, offs)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, SEED, k)
+    out = torch.full((count,), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins), steps, warmup)
+    t = float(np.mean(ms)) * 1e-3
+    res = {"input_offsets": offs, "kernel_ms_mean": round(t * 1e3, 4),
+           "achieved_GBps": round((n + 1) * count * 4 / t / 1e9, 1),
+           "frac": round((n + 1) * count * 4 / t / 1e9 / HBM_PEAK_GBPS, 4),
+           "parity_sample_ok": sample_check(out, n, count)}
+    del bases, ins, out
+    torch.cuda.empty_cache()
+    return res
 
 
 def c2variants(args):

@@ -12,9 +12,9 @@ tag=$1; shift
 out=gpurun_out/prof_$tag
 rm -rf "$out"; mkdir -p "$out"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o run -- \
-  python3 bench.py --no-cpu --steps 20 --warmup 5 "$@" > "$out/stats.log" 2>&1
+  python3 bench.py --no-cpu --no-misaligned --steps 20 --warmup 5 "$@" > "$out/stats.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- \
-  python3 bench.py --no-cpu --steps 5 --warmup 2 "$@" > "$out/fetch.log" 2>&1
+  python3 bench.py --no-cpu --no-misaligned --steps 5 --warmup 2 "$@" > "$out/fetch.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- \
-  python3 bench.py --no-cpu --steps 5 --warmup 2 "$@" > "$out/write.log" 2>&1
+  python3 bench.py --no-cpu --no-misaligned --steps 5 --warmup 2 "$@" > "$out/write.log" 2>&1
 ls -R "$out" | head -40
