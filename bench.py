@@ -278,6 +278,8 @@ def mix_ceiling(ins, out, count, reps=10, mode=0):
     probe.probe_run.argtypes = [ctypes.c_int] * 7 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                                      ctypes.c_uint64, ctypes.c_void_p]
     n = len(ins)
+    if n > 16:  # the probe kernels take at most 16 streams
+        return None
     tab = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ins])
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     best = 0.0
@@ -285,12 +287,12 @@ def mix_ceiling(ins, out, count, reps=10, mode=0):
         fn = lambda: probe.probe_run(mode, 256, 4, 2, 2, 0, grid, tab, n, ctypes.c_void_p(out.data_ptr()),  # noqa: E731
                                      count * 4, st)
         _, ms = time_launches(fn, reps, 3)
-        moved = (n + (1 if mode == 0 else 0)) * count * 4
+        moved = (n + 1 if mode == 0 else n if mode == 1 else 1) * count * 4
         best = max(best, moved / (np.median(ms) * 1e-3) / 1e9)
     return best
 
 
-def serial_rw_model(read_bytes, write_bytes, read_gbps, copy_gbps, kern_s):
+def serial_rw_model(read_bytes, write_bytes, read_gbps, copy_gbps, kern_s, write_gbps_probe=None):
     """The box's own HBM bound for a read/write mix: a DRAM channel either
     reads or writes, so a kernel that reads R and writes W bytes needs at
     least R / read_rate + W / write_rate.  read_rate = the 8-stream read-only
@@ -300,8 +302,15 @@ def serial_rw_model(read_bytes, write_bytes, read_gbps, copy_gbps, kern_s):
         return None
     write_gbps = 1.0 / (2.0 / copy_gbps - 1.0 / read_gbps)
     t = read_bytes / read_gbps / 1e9 + write_bytes / write_gbps / 1e9
-    return {"read_GBps": round(read_gbps, 1), "write_GBps_from_copy": round(write_gbps, 1),
-            "predicted_ms": round(t * 1e3, 4), "frac": round(t / kern_s, 4)}
+    m = {"read_GBps": round(read_gbps, 1), "write_GBps_from_copy": round(write_gbps, 1),
+         "predicted_ms": round(t * 1e3, 4), "frac": round(t / kern_s, 4)}
+    if write_gbps_probe:
+        # the same model with the write-only probe's rate (nt stores, no
+        # reads): the copy kernel's implied write rate is a pessimistic one
+        t2 = read_bytes / read_gbps / 1e9 + write_bytes / write_gbps_probe / 1e9
+        m.update({"write_GBps_probe": round(write_gbps_probe, 1), "predicted_ms_write_probe": round(t2 * 1e3, 4),
+                  "frac_write_probe": round(t2 / kern_s, 4)})
+    return m
 
 
 def copy_ceiling(nbytes=1 << 30, reps=10):
@@ -593,6 +602,7 @@ def main():
             log("bench: PARITY FAILURE against the oracle sample")
     mix_gbps = mix_ceiling(ins, out, count) if dist.rank == 0 else None
     read_gbps = mix_ceiling(ins, out, count, mode=1) if dist.rank == 0 else None
+    write_gbps = mix_ceiling(ins, out, count, mode=2) if dist.rank == 0 else None
     del ins, out
     torch.cuda.empty_cache()
 
@@ -616,7 +626,7 @@ def main():
     # HBM3E moves 4 bits per pin per reported memory clock (8 Gb/s per pin at
     # the 2 GHz the runtime reports on MI355X): 8192 bits -> 8.19 TB/s, the spec
     props_peak = 4.0 * mclk.value * 1e3 * bus.value / 8 / 1e9
-    serial = serial_rw_model(n * count * 4, count * 4, read_gbps, copy_gbps, kern_s)
+    serial = serial_rw_model(n * count * 4, count * 4, read_gbps, copy_gbps, kern_s, write_gbps)
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -724,6 +734,9 @@ def nway(args):
     copy_gbps = copy_ceiling()
     for n in (2, 3, 4, 8, 16, 32, 64):
       ins, out = make_bucket(n, count)
+      # the box's bound for this read/write mix on these very buckets
+      read_gbps = mix_ceiling(ins, out, count, mode=1)
+      write_gbps = mix_ceiling(ins, out, count, mode=2)
       for eng in (0, 1):  # auto (= phase at this size), tile
         cfg = dict(engine=eng) if eng else None
         _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins, config=cfg), args.steps, args.warmup)
@@ -733,7 +746,9 @@ def nway(args):
                           "kernel_ms": round(t * 1e3, 4),
                           "GBps": round(b / t / 1e9, 1), "frac_hbm": round(b / t / 1e9 / HBM_PEAK_GBPS, 4),
                           "read_GBps": round(n * count * 4 / t / 1e9, 1),
-                          "frac_of_copy": round(b / t / 1e9 / copy_gbps, 4)}), flush=True)
+                          "frac_of_copy": round(b / t / 1e9 / copy_gbps, 4),
+                          "serial_rw_model": serial_rw_model(n * count * 4, count * 4, read_gbps, copy_gbps, t, write_gbps)}),
+              flush=True)
       del ins, out
       torch.cuda.empty_cache()
     return 0
