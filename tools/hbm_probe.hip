@@ -108,6 +108,47 @@ __global__ __launch_bounds__(B) void k_mix_lds(Ptrs p) {
   }
 }
 
+// Grouped mix (mode 4, n <= 8): a workgroup reads G consecutive tiles (all
+// n inputs of a tile in flight, XOR into acc[g]) and stores the G tiles
+// together after the last one's reads, so its writes come in bursts of
+// G tiles.  G = 1 is the plain mix order.  nt loads and nt stores.
+template <int B, int U, int G>
+__global__ __launch_bounds__(B) void k_mix_grp(Ptrs p) {
+  const uint64_t tile = (uint64_t)B * U * 16;
+  const uint64_t ntiles = p.bytes / tile;
+  uint32_t voff[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) voff[u] = (u * B + threadIdx.x) * 16;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * G; t0 < ntiles; t0 += (uint64_t)gridDim.x * G) {
+    u32x4 acc[G][U];
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      const uint64_t off = (t0 + g) * tile;
+      const bool live = t0 + g < ntiles;
+      u32x4 x[8][U];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        rsrc_t r = mk(p.in[j < p.n ? j : 0] + (live ? off : 0), (live && j < p.n) ? (uint32_t)tile : 0u);
+#pragma unroll
+        for (int u = 0; u < U; u++) x[j][u] = __builtin_amdgcn_raw_buffer_load_b128(r, voff[u], 0, 2);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        acc[g][u] = x[0][u];
+#pragma unroll
+        for (int j = 1; j < 8; j++) acc[g][u] ^= x[j][u];
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      const bool live = t0 + g < ntiles;
+      rsrc_t w = mk(p.out + (live ? (t0 + g) * tile : 0), live ? (uint32_t)tile : 0u);
+#pragma unroll
+      for (int u = 0; u < U; u++) __builtin_amdgcn_raw_buffer_store_b128(acc[g][u], w, voff[u], 0, 2);
+    }
+  }
+}
+
 template <class K>
 static int launch(K kern, int grid, int block, Ptrs p, hipStream_t s) {
   hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, s, p);
@@ -172,6 +213,19 @@ int probe_run(int mode, int block, int unroll, int aux_load, int aux_store, int 
   p.bytes = bytes;
   p.n = n;
   hipStream_t s = (hipStream_t)stream;
+  if (mode == 4) {  // grouped mix: unroll = U, order = G
+    if (n > 8 || block != 256) return -1;
+    const int key = unroll * 10 + order;
+    switch (key) {
+      case 41: return launch(k_mix_grp<256, 4, 1>, grid, 256, p, s);
+      case 42: return launch(k_mix_grp<256, 4, 2>, grid, 256, p, s);
+      case 22: return launch(k_mix_grp<256, 2, 2>, grid, 256, p, s);
+      case 24: return launch(k_mix_grp<256, 2, 4>, grid, 256, p, s);
+      case 14: return launch(k_mix_grp<256, 1, 4>, grid, 256, p, s);
+      case 18: return launch(k_mix_grp<256, 1, 8>, grid, 256, p, s);
+    }
+    return -1;
+  }
   if (mode == 3) {
     if (block == 256) return aux_load ? launch(k_mix_lds<256, 2>, grid, 256, p, s)
                                       : launch(k_mix_lds<256, 0>, grid, 256, p, s);
