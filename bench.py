@@ -488,6 +488,7 @@ def traffic_from_profiles(n, count, kernel=DEFAULT_KERNEL):
             except (OSError, ValueError):
                 continue
             if (d.get("n_inputs") == n and d.get("count") == count and d.get("hbm_bytes_per_launch")
+                    and not d.get("variant")  # e.g. the misaligned-input run: not the headline's buckets
                     and kernel and kernel in d.get("kernel", "")):
                 best = d
     return best
