@@ -45,7 +45,7 @@ ABI_LINK = -Lhiccl_amd -lhiccl_reduce -Wl,-rpath,'$$ORIGIN/../hiccl_amd' -L/opt/
 HDRS = include/hiccl.h $(wildcard include/hiccl/*.h) include/hiccl_reduce.h hiccl_amd/csrc/compose.h
 
 CPP_BINS = build/plan_dump build/collectives_host build/collectives_host_f32 build/collectives_hip build/collectives_hip_f32 \
-           build/readme_example_host build/readme_example_hip build/abi_c
+           build/readme_example_host build/readme_example_hip build/abi_c build/ipc_reuse
 
 cpp: $(CPP_BINS)
 
@@ -76,6 +76,11 @@ build/readme_example_host: hiccl_amd/csrc/readme_example.cpp $(HDRS)
 build/readme_example_hip: hiccl_amd/csrc/readme_example.cpp $(HDRS) $(LIB)
 	@mkdir -p build
 	$(CXX) $(CXXFLAGS) $(HIP_HOST) -o $@ $< $(HIP_LINK) $(MPI_LINK)
+
+# two-process reproducer of the IPC close/reopen behaviour (tests/test_ipc_reuse_gpu.py)
+build/ipc_reuse: tests/cpp/ipc_reuse.cpp include/hiccl_reduce.h $(LIB)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o $@ $< $(ABI_LINK) $(MPI_LINK)
 
 # plain C99 client of the C ABI (the header must stay C)
 build/abi_c: tests/cpp/abi_c.c include/hiccl_reduce.h $(LIB)

@@ -144,9 +144,15 @@ def run_c5(world, args, allow_shared=False):
     1-GPU box, tests/test_c5_leg_gpu.py; the library then runs host-driven)."""
     import shutil
     import tempfile
-    ndev = torch.cuda.device_count()  # (does not initialise HIP)
+    # the MPI ranks pick their GPU by local rank (CommBench::init); a per-rank
+    # device mask inherited from this torchrun rank would show them one GPU
+    # each and put every rank on it -- drop the masks from the job's
+    # environment and say which were dropped
+    base_env, scrubbed = c5_child_env(os.environ)
+    ndev = visible_gpus(base_env)
     if ndev < world and not allow_shared:
-        return {"skipped": f"{world} ranks on {ndev} GPU(s): config 5 needs one GPU per rank"}
+        return {"skipped": f"{world} ranks on {ndev} GPU(s): config 5 needs one GPU per rank",
+                "env_scrubbed": scrubbed, "devices_counted_unmasked": ndev}
     if not os.path.exists(C5_EXE):
         return {"skipped": f"{C5_EXE} not built"}
     mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
@@ -154,14 +160,16 @@ def run_c5(world, args, allow_shared=False):
     libs = "mpi,ipc,ipc" if hier.count(",") == 2 else "ipc"
     count = 1 << args.c5_log2count
     out = {"workload": f"C5: all-reduce of {count * world * 4 >> 20} MiB fp32 per rank, {world} ranks, hierarchy "
-                       f"{{{hier}}} {{{libs}}}, pipedepth 128 (collectives/main.cpp:151-155)"}
+                       f"{{{hier}}} {{{libs}}}, pipedepth 128 (collectives/main.cpp:151-155)",
+           "env_scrubbed": scrubbed, "devices_counted_unmasked": ndev}
     fused = {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "1"}
     modes = [("host", {"HICCL_STREAM_ORDERED": "0"}, hier, libs),
              ("stream_graph", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "0"}, hier, libs),
              ("stream_graph_fused", fused, hier, libs)]
     # the reference's main.cu runs its levels on XCCL (main.cu:25): RCCL
-    # point-to-point per level (on shared GPUs the library falls back to IPC)
-    modes.append(("xccl", {"HICCL_STREAM_ORDERED": "0"}, hier, libs.replace("ipc", "xccl")))
+    # point-to-point per level, opted into here (HICCL_XCCL=rccl; on shared
+    # GPUs the library falls back to IPC, and mode_used says which ran)
+    modes.append(("xccl", {"HICCL_STREAM_ORDERED": "0", "HICCL_XCCL": "rccl"}, hier, libs.replace("ipc", "xccl")))
     if hier != str(world):
         # not the reference's config: the same all-reduce on one flat IPC
         # level, every peer over its own xGMI link of the full mesh ({1,4,2}
@@ -177,7 +185,7 @@ def run_c5(world, args, allow_shared=False):
             continue
         fd, path = tempfile.mkstemp(prefix="hiccl_c5_", suffix=".json", dir="/tmp")
         os.close(fd)
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_DRIVER_JSON=path, OMP_NUM_THREADS="1",
+        env = dict(base_env, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_DRIVER_JSON=path, OMP_NUM_THREADS="1",
                    HICCL_SIGNAL_TIMEOUT="20", **extra)
         if ndev < world:
             # a rehearsal with ranks sharing GPUs: HIP's 4 hardware queues per
@@ -201,6 +209,30 @@ def run_c5(world, args, allow_shared=False):
         if p.returncode != 0:
             break  # a failure, crash or time-out: start nothing more on the GPUs
     return out
+
+
+DEVICE_MASKS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL")
+
+
+def c5_child_env(env):
+    """The config-5 MPI job's environment: `env` without per-process GPU
+    masks.  Returns (env, {mask: dropped value})."""
+    child = dict(env)
+    dropped = {k: child.pop(k) for k in DEVICE_MASKS if k in child}
+    return child, dropped
+
+
+def visible_gpus(env):
+    """GPUs a process started with `env` sees (hipGetDeviceCount in a child,
+    so this process's HIP state and device mask do not matter); 0 if none."""
+    code = ("import ctypes\n"
+            "try:\n h = ctypes.CDLL('libamdhip64.so')\nexcept OSError:\n h = ctypes.CDLL('/opt/rocm/lib/libamdhip64.so')\n"
+            "n = ctypes.c_int(0)\nprint(n.value if h.hipGetDeviceCount(ctypes.byref(n)) == 0 else 0)\n")
+    try:
+        p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        return int(p.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError, OSError):
+        return 0
 
 
 def whole_job_gbps(world, bytes_per_step, steps, wall_max_s):
@@ -650,7 +682,21 @@ def main():
                      # the HBM-read view: the n input reads only
                      "read_achieved_GBps": round(n * count * 4 / kern_s / 1e9, 1),
                      "read_frac": round(n * count * 4 / kern_s / 1e9 / HBM_PEAK_GBPS, 4),
+                     # the read view against what this box's HBM delivers to a
+                     # read-only 8-stream probe on the same buckets
+                     "read_frac_of_read_ceiling": round(n * count * 4 / kern_s / 1e9 / read_gbps, 4)
+                     if read_gbps else None,
+                     # PMC bytes per launch of this kernel on this workload from a
+                     # committed rocprofv3 profile (traffic_source), not counted in
+                     # this run: bench.py does not run under rocprofv3
                      "traffic": (prof or {}).get("hbm_bytes_per_launch"),
+                     "traffic_from_profile": (
+                         {"tag": prof.get("tag"), "file": f"profiles/{prof.get('tag')}_pmc.json",
+                          "box_kernel_ms": round(prof["rocprof_avg_kernel_ns"] * 1e-6, 4)
+                          if prof.get("rocprof_avg_kernel_ns") else None,
+                          "over_algorithmic": round(prof["traffic_over_algorithmic"], 5)
+                          if prof.get("traffic_over_algorithmic") else None,
+                          "measured_in_this_run": False} if prof else None),
                      "kernel_ms_mean": round(kern_s * 1e3, 4), "kernel_ms_min": round(min(kms), 4),
                      "kernel_ms_median": round(float(np.median(kms)), 4), "kernel_ms_max": round(max(kms), 4),
                      "mix_ceiling_GBps": round(mix_gbps, 1) if mix_gbps else None,
@@ -904,26 +950,77 @@ def crossover(args):
 
 
 def c2_misaligned(n, count, steps, warmup):
-    """SURVEY.md 8d's second C2 run: the same bucket with input k placed
-    1 + k mod 3 elements past a 16-B boundary (the mutual misalignment
-    partition() produces, reduce.h:401-415), output aligned; fresh buffers,
-    the headline's steps/warmup, a sampled bitwise check."""
+    """SURVEY.md 8d's second C2 run, as an interleaved A/B on ONE set of
+    allocations: input k is read either from its 16-B-aligned base or from
+    1 + k mod 3 elements past it (the mutual misalignment partition()
+    produces, reduce.h:401-415), output aligned; launches alternate between
+    the two views so placement and box state are common to both.  A sampled
+    bitwise check of each view's output against the oracle generator."""
     offs = [1 + k % 3 for k in range(n)]
     bases = [torch.empty(count + 4, dtype=torch.float32, device="cuda") for _ in range(n)]
-    ins = [b[o:o + count] for b, o in zip(bases, offs)]
-    for k, t in enumerate(ins):
-        hiccl_amd.fill_uniform(t, SEED, k)
-    out = torch.full((count,), float("nan"), dtype=torch.float32, device="cuda")
+    for k, b in enumerate(bases):  # element j of base k = generator(k, j), shifted views included
+        hiccl_amd.fill_uniform(b, SEED, k)
+    aligned = [b[:count] for b in bases]
+    shifted = [b[o:o + count] for b, o in zip(bases, offs)]
+    out = torch.empty(count, dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
-    _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins), steps, warmup)
-    t = float(np.mean(ms)) * 1e-3
-    res = {"input_offsets": offs, "kernel_ms_mean": round(t * 1e3, 4),
-           "achieved_GBps": round((n + 1) * count * 4 / t / 1e9, 1),
-           "frac": round((n + 1) * count * 4 / t / 1e9 / HBM_PEAK_GBPS, 4),
-           "parity_sample_ok": sample_check(out, n, count)}
-    del bases, ins, out
+    s = torch.cuda.current_stream()
+    runs = {"aligned": lambda: hiccl_amd.reduce(out, aligned), "shifted": lambda: hiccl_amd.reduce(out, shifted)}
+    for _ in range(warmup):
+        for fn in runs.values():
+            fn()
+    torch.cuda.synchronize()
+    ms = {k: [] for k in runs}
+    for _ in range(steps):
+        for k, fn in runs.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            fn()
+            b.record(s)
+            ms[k].append((a, b))
+    torch.cuda.synchronize()
+    t = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e-3 for k, v in ms.items()}
+    parity = {}
+    for k, fn in runs.items():
+        fn()
+        torch.cuda.synchronize()
+        parity[k] = sample_check_shifted(out, [0] * n if k == "aligned" else offs, count)
+    bytes_step = (n + 1) * count * 4
+    res = {"ab": "interleaved launches on the same allocations", "input_offsets": offs,
+           "aligned_kernel_ms_mean": round(t["aligned"] * 1e3, 4), "shifted_kernel_ms_mean": round(t["shifted"] * 1e3, 4),
+           "shifted_over_aligned": round(t["shifted"] / t["aligned"], 4),
+           "aligned_GBps": round(bytes_step / t["aligned"] / 1e9, 1),
+           "shifted_GBps": round(bytes_step / t["shifted"] / 1e9, 1),
+           "shifted_frac": round(bytes_step / t["shifted"] / 1e9 / HBM_PEAK_GBPS, 4),
+           "parity_sample_ok": parity}
+    del bases, aligned, shifted, out
     torch.cuda.empty_cache()
     return res
+
+
+def sample_check_shifted(out, offs, count, seed=SEED, nsample=512):
+    """Bitwise check of out[i] = (((0 + g(0, i + offs[0])) + g(1, i + offs[1]))
+    + ...) at random i, g = the oracle generator (oracle_fill_uniform_f32
+    at a start index)."""
+    ora_so = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not os.path.exists(ora_so):
+        return None
+    ora = ctypes.CDLL(ora_so)
+    fill = ora.oracle_fill_uniform_f32
+    fill.restype = None
+    fill.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t]
+    idx = np.random.default_rng(1).integers(0, count, nsample)
+    idx[:2] = [0, count - 1]
+    exp = np.zeros(nsample, np.float32)
+    v = np.empty(1, np.float32)
+    for k, o in enumerate(offs):
+        col = np.empty(nsample, np.float32)
+        for j, i in enumerate(idx):
+            fill(v.ctypes.data, 1, seed, k, int(i) + o)
+            col[j] = v[0]
+        exp = (exp + col).astype(np.float32)  # one f32 add per input, in input order
+    got = out[torch.from_numpy(idx.astype(np.int64)).to(out.device)].cpu().numpy()
+    return bool(np.array_equal(got.view(np.uint32), exp.view(np.uint32)))
 
 
 def c2variants(args):

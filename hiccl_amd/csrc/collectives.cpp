@@ -16,6 +16,7 @@
 //
 // Element type: size_t (as the reference driver, collectives/main.cpp:24) or
 // float with -DHICCL_DRIVER_FLOAT.
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -73,6 +74,9 @@ static inline float uniform_f32(uint64_t seed, uint32_t k, uint64_t i) {
   return (float)(uint32_t)(h >> 40) * (1.0f / 8388608.0f) - 1.0f;
 }
 
+// The known-answer pattern times `ranks`: ranks * ((i mod 1021) - 510).
+static inline int64_t kat_value(size_t i, int ranks) { return (int64_t)ranks * ((int64_t)(i % 1021) - 510); }
+
 // HICCL_DRIVER_JSON=<path> (rank 0 writes it): HiCCL::measure of the whole
 // collective (bench.h:2-60 semantics: barrier, run, MAX over ranks), the
 // per-step kernel time of each rank's batched compute (HIP events; MAX over
@@ -86,7 +90,10 @@ static int bench_json(const char *path, HiCCL::Comm<Type> &coll, Type *sendbuf_d
   const int myid = CommBench::myid, numproc = CommBench::numproc;
   const size_t n = count * numproc;
   std::vector<Type> host(n);
-  for (size_t i = 0; i < n; i++) host[i] = (Type)((double)(i % 1021) - 510.0);
+  // built as a signed integer, then converted: a negative double converted
+  // to the unsigned driver type (size_t) would be undefined behaviour, the
+  // int64_t -> size_t conversion wraps (and the expected sums wrap alike)
+  for (size_t i = 0; i < n; i++) host[i] = (Type)kat_value(i, 1);
   CommBench::memcpyH2D(sendbuf_d, host.data(), n);
   double kern_ms = 0, kern_bytes = 0;
   int ksteps = 0;
@@ -114,10 +121,43 @@ static int bench_json(const char *path, HiCCL::Comm<Type> &coll, Type *sendbuf_d
   size_t bad = 0;
   if (pattern == HiCCL::allreduce)
     for (size_t i = 0; i < n; i++)
-      if (out[i] != (Type)(numproc * ((double)(i % 1021) - 510.0))) bad++;
+      if (out[i] != (Type)kat_value(i, numproc)) bad++;
   unsigned long tot = bad;
   MPI_Allreduce(MPI_IN_PLACE, &tot, 1, MPI_UNSIGNED_LONG, MPI_SUM, CommBench::comm_mpi);
+  // where the ranks ran: every rank's visible device count, its device and
+  // that device's PCI bus id (a per-rank device mask that hid the other GPUs
+  // shows as devices_seen 1 and repeated bus ids)
+  char where[64];
+  std::memset(where, 0, sizeof(where));
+#ifndef HICCL_PORT_HOST
+  {
+    int ndev = 0;
+    (void)hipGetDeviceCount(&ndev);
+    char bus[32] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, CommBench::mydevice) != hipSuccess) std::strcpy(bus, "?");
+    std::snprintf(where, sizeof(where), "%d|%d|%s", ndev, CommBench::mydevice, bus);
+  }
+#else
+  std::snprintf(where, sizeof(where), "0|-1|host");
+#endif
+  std::vector<char> wall((size_t)numproc * sizeof(where));
+  MPI_Gather(where, sizeof(where), MPI_CHAR, wall.data(), sizeof(where), MPI_CHAR, 0, CommBench::comm_mpi);
   if (myid == 0) {
+    std::string seen, devs, buses;
+    for (int r = 0; r < numproc; r++) {
+      std::string w(wall.data() + (size_t)r * sizeof(where));
+      const size_t a = w.find('|'), b = w.find('|', a + 1);
+      seen += (r ? "," : "") + w.substr(0, a);
+      devs += (r ? "," : "") + w.substr(a + 1, b - a - 1);
+      buses += std::string(r ? ", " : "") + "\"" + w.substr(b + 1) + "\"";
+    }
+    std::string mode_used = coll.stream_ordered() ? "stream-ordered" : "host-driven";
+    if (coll.graph_mode()) mode_used += "+graph";
+    if (coll.fused_gather()) mode_used += "+fused";
+#ifndef HICCL_PORT_HOST
+    if (coll.xccl_on_rccl()) mode_used += "+xccl-rccl";
+    if (coll.shares_device()) mode_used += " (ranks share a GPU)";
+#endif
     std::string h, l;
     for (size_t i = 0; i < hierarchy.size(); i++) h += (i ? "," : "") + std::to_string(hierarchy[i]);
     for (size_t i = 0; i < libs.size(); i++) l += std::string(i ? "," : "") + CommBench::lib_name(libs[i]);
@@ -131,12 +171,14 @@ static int bench_json(const char *path, HiCCL::Comm<Type> &coll, Type *sendbuf_d
                  "\"collective_ms_max\": %.4f, \"algorithmic_GBps_median\": %.2f, "
                  "\"kernel_steps_rank0\": %d, \"kernel_ms_per_run_max_rank\": %.4f, "
                  "\"kernel_us_per_step_rank0\": %.3f, \"kernel_GBps_max_rank\": %.1f, "
-                 "\"kat_exact_mismatches\": %lu, \"kat\": \"%s\"}\n",
+                 "\"kat_exact_mismatches\": %lu, \"kat\": \"%s\", \"devices_seen\": [%s], \"rank_devices\": [%s], "
+                 "\"bus_ids\": [%s], \"mode_used\": \"%s\"}\n",
                  numproc, pattern, h.c_str(), l.c_str(), pipedepth, count, data, coll.stream_ordered() ? "stream-ordered" : "host-driven",
                  coll.graph_mode() ? "+graph" : "", coll.fused_gather() ? "+fused" : "", t.t.size(), t.min() * 1e3,
                  t.median() * 1e3, t.max() * 1e3, t.median() > 0 ? data / t.median() / 1e9 : 0.0, ksteps, kmax[0],
                  ksteps ? kern_ms / ksteps * 1e3 : 0.0, kmax[0] > 0 ? kmax[1] / (kmax[0] * 1e-3) / 1e9 : 0.0, tot,
-                 pattern != HiCCL::allreduce ? "n/a" : tot == 0 ? "PASSED" : "FAILED");
+                 pattern != HiCCL::allreduce ? "n/a" : tot == 0 ? "PASSED" : "FAILED", seen.c_str(), devs.c_str(),
+                 buses.c_str(), mode_used.c_str());
     std::fclose(f);
   }
   return tot == 0 ? 0 : 1;

@@ -969,9 +969,13 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
 // four: n = 2 at 1-2 GiB per input 6.50-6.66 vs 6.33-6.46 TB/s at 8; n = 3 / 4
 // lead at 8, profiles/r02g_wideverify.jsonl), or 0.  f32 / bf16 native only,
 // from kWideMinTicketsPerWG 8-packet tiles per workgroup (1 GiB per input).
-int auto_wide_unroll(uint64_t npkt, double n, int dtype, int acc, int dev) {
-  const bool tuned = dtype == HICCL_FLOAT32 || (dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_NATIVE);
+// Wide tiles exist only at block 256 with nt loads and nt stores (pick_u):
+// a caller that asks for another block or cache policy keeps the u4 / PHASE
+// choice instead of an unsupported shape.
+int auto_wide_unroll(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
+  const bool tuned = dtype == HICCL_FLOAT32 || (dtype == HICCL_BFLOAT16 && c.acc == HICCL_ACC_NATIVE);
   if (!tuned || n < 1.5 || n >= kDynMinInputs) return 0;
+  if ((c.block && c.block != kDefBlock) || c.nt != kDefPol % 10 || c.store != kDefPol / 10) return 0;
   if (npkt / ((uint64_t)kDefBlock * kWideUnroll) < kWideMinTicketsPerWG * (uint64_t)device_cus(dev)) return 0;
   return n < 2.5 ? 2 * kWideUnroll : kWideUnroll;
 }
@@ -985,8 +989,9 @@ int auto_wide_unroll(uint64_t npkt, double n, int dtype, int acc, int dev) {
 // (n = 8, 128 MiB = 32 tickets: 6.41 vs 5.94); with <= 4 inputs the phased
 // engine leads at every size with a chunk per CU (r01_schedsweep.jsonl) --
 // except from 1 GiB per input, where wide tiles lead (auto_wide_unroll).
-int auto_engine(uint64_t npkt, double n, int dtype, int acc, int dev) {
-  if (auto_wide_unroll(npkt, n, dtype, acc, dev)) return HICCL_ENGINE_TILE;
+int auto_engine(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
+  const int acc = c.acc;
+  if (auto_wide_unroll(npkt, n, dtype, c, dev)) return HICCL_ENGINE_TILE;
   const bool packed_ok = !(dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_WIDE);
   if (n >= kDynMinInputs && packed_ok) {
     const uint64_t tickets = npkt / ((uint64_t)kDefBlock * kDefUnroll) / default_grab(HICCL_ENGINE_TILE, n);
@@ -1026,14 +1031,14 @@ int auto_unroll(uint64_t npkt, int dtype, int acc, int dev) {
 // packet-weighted mean).
 void finish_cfg(Cfg &c, uint64_t npkt, double n, int dtype, int dev) {
   if (c.engine == HICCL_ENGINE_AUTO)
-    c.engine = (c.block || c.unroll) ? HICCL_ENGINE_TILE : auto_engine(npkt, n, dtype, c.acc, dev);
+    c.engine = (c.block || c.unroll) ? HICCL_ENGINE_TILE : auto_engine(npkt, n, dtype, c, dev);
   if (c.engine == HICCL_ENGINE_PHASE) {
     if (!c.block) c.block = kPhBlock;
     if (!c.unroll) c.unroll = phase_p_dtype(dtype, c.acc);
   } else {
     if (!c.block) c.block = kDefBlock;
     if (!c.unroll) {
-      const int wide = auto_wide_unroll(npkt, n, dtype, c.acc, dev);
+      const int wide = auto_wide_unroll(npkt, n, dtype, c, dev);
       c.unroll = wide ? wide : auto_unroll(npkt, dtype, c.acc, dev);
     }
   }
@@ -1586,27 +1591,41 @@ int hiccl_reduce_plan_add(hiccl_reduce_plan_t *p, void *out, const void *const *
   return 0;
 }
 
-int hiccl_reduce_plan_enqueue(hiccl_reduce_plan_t *p, void *stream) {
-  if (!p) return fail(hipErrorInvalidValue, "plan_enqueue: plan is NULL");
-  if (int e = check_hip(hipSetDevice(p->device), "plan_enqueue: hipSetDevice")) return e;
+}  // extern "C"
+
+namespace {
+// Upload (if needed) and launch, no bookkeeping of where the launch went.
+int plan_enqueue_impl(hiccl_reduce_plan_t *p, hipStream_t s, const char *what) {
+  if (!p) return fail(hipErrorInvalidValue, std::string(what) + ": plan is NULL");
+  if (int e = check_hip(hipSetDevice(p->device), (std::string(what) + ": hipSetDevice").c_str())) return e;
   if (p->comps.empty()) return 0;
-  hipStream_t s = (hipStream_t)stream;
   if (int e = plan_upload(p, s)) return e;
-  if (int e = plan_kernel(p, s)) return e;
+  return plan_kernel(p, s);
+}
+}  // namespace
+
+extern "C" {
+
+int hiccl_reduce_plan_enqueue(hiccl_reduce_plan_t *p, void *stream) {
+  if (int e = plan_enqueue_impl(p, (hipStream_t)stream, "plan_enqueue")) return e;
   // no stream bookkeeping (callers on several threads and streams); a
   // re-upload or destroy then synchronises the device before it frees the
   // block a launch may still read
-  p->enqueued.store(true, std::memory_order_relaxed);
+  if (!p->comps.empty()) p->enqueued.store(true, std::memory_order_relaxed);
   return 0;
 }
 
 int hiccl_reduce_plan_launch(hiccl_reduce_plan_t *p, void *stream) {
-  if (int e = hiccl_reduce_plan_enqueue(p, stream)) return e;
-  if (p->comps.empty()) return 0;
   hipStream_t s = (hipStream_t)stream;
+  if (int e = plan_enqueue_impl(p, s, "plan_launch")) return e;
+  if (p->comps.empty()) return 0;
   // a capturing stream is not remembered (plan_sync does not apply to graph
-  // replays: synchronise the stream the graph runs on)
-  if (capturing(s, false)) return 0;
+  // replays: synchronise the stream the graph runs on); a re-upload or
+  // destroy of a plan captured into a graph synchronises the device
+  if (capturing(s, false)) {
+    p->enqueued.store(true, std::memory_order_relaxed);
+    return 0;
+  }
   p->launched = true;
   p->last = s;
   return 0;
@@ -1633,7 +1652,11 @@ int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *p) {
   // the reference's wait(): hipStreamSynchronize of the compute's stream
   // (compute.h:107-117) -- no completion event per launch (an event record
   // after every kernel costs the queue ~3 us per step on MI355X)
-  return check_hip(hipStreamSynchronize(p->last), "plan_sync");
+  if (int e = check_hip(hipStreamSynchronize(p->last), "plan_sync")) return e;
+  // nothing of this plan is pending on that stream any more: a later
+  // re-upload or destroy does not touch it (the caller may destroy it)
+  p->launched = false;
+  return 0;
 }
 
 int hiccl_reduce_plan_numcomp(const hiccl_reduce_plan_t *p) { return p ? (int)p->comps.size() : 0; }

@@ -236,7 +236,8 @@ class Comm {
       if (!xccl && CommBench::myid == CommBench::printid)
         std::printf("HiCCL: XCCL levels run on the IPC path (%s)\n",
 #ifdef HICCL_WITH_RCCL
-                    "ranks share a GPU: RCCL needs one GPU per rank"
+                    !CommBench::xccl_rccl_requested() ? "RCCL is opt-in: HICCL_XCCL=rccl"
+                                                      : "ranks share a GPU: RCCL needs one GPU per rank"
 #else
                     "built without HICCL_WITH_RCCL"
 #endif
@@ -279,6 +280,7 @@ class Comm {
   }
 
   bool xccl_on_rccl() const { return xccl; }
+  bool shares_device() const { return shared_device; }  // two or more ranks drive one GPU (init)
 
   bool stream_ordered() const { return streamed; }
   bool fused_gather() const { return fused; }
@@ -539,6 +541,9 @@ class Comm {
     if (!fin) MPI_Barrier(CommBench::comm_mpi);  // every peer has released its mappings of this rank's buffers
 #endif
     for (T *p : owned) CommBench::free(p);
+#ifndef HICCL_PORT_HOST
+    if (xccl) CommBench::xccl_release();  // the last RCCL user destroys the communicator
+#endif
   }
 
  private:

@@ -17,9 +17,10 @@
 //                  host memory (MPICH here is not GPU-aware)
 //   XCCL           RCCL point-to-point (ncclSend/ncclRecv in one group per
 //                  step on the transport stream) when built with
-//                  HICCL_WITH_RCCL and every rank drives its own GPU
-//                  (RCCL refuses two ranks on one device); otherwise the
-//                  level runs on the IPC path and init() says so
+//                  HICCL_WITH_RCCL, asked for with HICCL_XCCL=rccl, and
+//                  every rank drives its own GPU (RCCL refuses two ranks on
+//                  one device); otherwise the level runs on the IPC path and
+//                  init() says so
 //   dummy          nothing
 //
 // Host port (HICCL_PORT_HOST, config 1: no GPU): buffers are host memory and
@@ -169,11 +170,32 @@ inline void nccl_check(ncclResult_t e, const char *what) {
   if (e != ncclSuccess) die(what, ncclGetErrorString(e));
 }
 #endif
+// HICCL_XCCL=rccl opts the XCCL levels into RCCL.  Until a run with one GPU
+// per rank has passed the known-answer test the RCCL path is not the
+// default: XCCL levels take the (tested) xGMI IPC path unless asked.
+inline bool xccl_rccl_requested() {
+  const char *e = std::getenv("HICCL_XCCL");
+  return e && std::string(e) == "rccl";
+}
+
+// Communicators whose XCCL levels run on RCCL; the last one to go destroys
+// the RCCL communicator (xccl_release), so ncclCommDestroy runs before
+// MPI_Finalize in every driver that scopes its HiCCL::Comm.
+inline int &xccl_users() {
+  static int n = 0;
+  return n;
+}
+
 // Collective.  Returns whether XCCL levels run on RCCL; otherwise they run
-// on the IPC path (no RCCL in this build, or ranks sharing a device).
+// on the IPC path (not requested, no RCCL in this build, or ranks sharing a
+// device).  A true return must be paired with xccl_release().
 inline bool xccl_setup(bool shared_device) {
 #ifdef HICCL_WITH_RCCL
-  if (xccl_on()) return true;
+  if (!xccl_rccl_requested()) return false;
+  if (xccl_on()) {
+    xccl_users()++;
+    return true;
+  }
   if (shared_device) return false;
   ncclUniqueId id;
   if (myid == 0) nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
@@ -181,10 +203,23 @@ inline bool xccl_setup(bool shared_device) {
   setup_gpu();
   nccl_check(ncclCommInitRank(&xccl_comm(), numproc, id, myid), "ncclCommInitRank");
   xccl_on() = true;
+  xccl_users() = 1;
   return true;
 #else
   (void)shared_device;
   return false;
+#endif
+}
+
+// Drop one user of the RCCL communicator; the last destroys it (after the
+// caller has synchronised every stream RCCL work was enqueued on).
+inline void xccl_release() {
+#ifdef HICCL_WITH_RCCL
+  if (!xccl_on() || --xccl_users() > 0) return;
+  setup_gpu();
+  (void)ncclCommDestroy(xccl_comm());
+  xccl_comm() = nullptr;
+  xccl_on() = false;
 #endif
 }
 
@@ -221,15 +256,40 @@ inline const char *lib_name(library lib) {
 
 inline void print_lib(library lib) { std::printf("%s", lib_name(lib)); }
 
+#ifndef HICCL_PORT_HOST
+inline size_t &ipc_retired_bytes();
+inline size_t ipc_retired_max();
+#endif
+
+// Collective.  Bytes allocated through allocate() over all ranks, and (HIP
+// port) the peers' freed allocations this process's retired IPC mappings
+// still keep alive (see IpcMapping) with their cap, largest rank.
 inline void report_memory() {
-  std::vector<size_t> all(numproc);
-  MPI_Allgather(&memory, sizeof(size_t), MPI_BYTE, all.data(), sizeof(size_t), MPI_BYTE, comm_mpi);
+  size_t mine[3] = {memory, 0, 0};
+#ifndef HICCL_PORT_HOST
+  mine[1] = ipc_retired_bytes();
+  mine[2] = ipc_retired_max();
+#endif
+  std::vector<size_t> all((size_t)numproc * 3);
+  MPI_Allgather(mine, sizeof(mine), MPI_BYTE, all.data(), sizeof(mine), MPI_BYTE, comm_mpi);
   if (myid == printid) {
-    size_t tot = 0;
-    for (int p = 0; p < numproc; p++) tot += all[p];
+    size_t tot = 0, ret = 0, cap = 0;
+    for (int p = 0; p < numproc; p++) {
+      tot += all[3 * p];
+      ret = std::max(ret, all[3 * p + 1]);
+      cap = std::max(cap, all[3 * p + 2]);
+    }
     std::printf("CommBench memory: ");
     print_data(tot);
-    std::printf(" total over %d ranks\n", numproc);
+    std::printf(" total over %d ranks", numproc);
+#ifndef HICCL_PORT_HOST
+    std::printf("; retired IPC mappings keep ");
+    print_data(ret);
+    std::printf(" of peer memory alive (largest rank; cap ");
+    print_data(cap);
+    std::printf(")");
+#endif
+    std::printf("\n");
   }
 }
 
@@ -310,14 +370,17 @@ struct IpcExport {
 // (measured: 4 ranks x 5 recreated communicators on reallocated buffers fail
 // within 1-3 runs when mappings are closed, never when they stay open; a
 // 200 ms pause after the close does not help; tests/test_mpi_gpu.py
-// ::test_recreated_communicators_on_reallocated_buffers).  A retired
-// mapping is revived when the peer exports the same allocation again (same
-// base, not recycled) and closed, oldest first, only when the retired
-// mappings exceed HICCL_IPC_RETIRED_MAX bytes (default: a quarter of the
-// device's memory; they keep the peers' freed allocations alive) or on
-// ipc_trim().  A mapping opened for a recycled address is verified by a
-// probe (ipc_probe_*), so a closed-then-reopened address that misses fails
-// loudly instead of losing data.
+// ::test_recreated_communicators_on_reallocated_buffers; the two-process
+// reproducer tests/cpp/ipc_reuse.cpp, tests/test_ipc_reuse_gpu.py).  A
+// retired mapping is revived when the peer exports the same allocation
+// again (same base, not recycled) and closed, oldest first, only when the
+// retired mappings exceed the cap or on ipc_trim().  The cap
+// (HICCL_IPC_RETIRED_MAX bytes) defaults to twice the largest set of peer
+// allocations this process has had mapped at once: at most two generations
+// of a communicator's peer buffers stay alive after they are freed, never
+// more than a fixed share of HBM.  A mapping opened for a recycled address is
+// verified by a probe (ipc_probe_*), so a closed-then-reopened address that
+// misses fails loudly instead of losing data.
 struct IpcMapping {
   char *ptr;
   int refs;
@@ -342,17 +405,23 @@ inline size_t &ipc_retired_bytes() {
   static size_t b = 0;
   return b;
 }
+// Bytes of peer allocations mapped (live, not retired) right now, and the
+// most there ever were at once.
+inline size_t &ipc_live_bytes() {
+  static size_t b = 0;
+  return b;
+}
+inline size_t &ipc_live_peak() {
+  static size_t b = 0;
+  return b;
+}
 inline size_t ipc_retired_max() {
-  static const size_t cap = [] {
-    if (const char *e = std::getenv("HICCL_IPC_RETIRED_MAX")) return (size_t)std::strtoull(e, nullptr, 0);
-    size_t fr = 0, total = 0;
-    if (hipMemGetInfo(&fr, &total) != hipSuccess) {
-      (void)hipGetLastError();
-      return (size_t)16 << 30;
-    }
-    return total / 4;
+  static const long long env = [] {
+    const char *e = std::getenv("HICCL_IPC_RETIRED_MAX");
+    return e ? (long long)std::strtoull(e, nullptr, 0) : -1ll;
   }();
-  return cap;
+  if (env >= 0) return (size_t)env;
+  return 2 * ipc_live_peak();
 }
 
 // HICCL_DEBUG_IPC=1: every export, import and close on stdout; =2: kept in
@@ -445,6 +514,10 @@ inline uint64_t ipc_probe_begin(IpcExport &e, void *p, size_t bytes) {
   uint64_t saved = 0;
   e.probe = (uint32_t)std::min<size_t>(bytes, 8);
   if (!e.probe) return 0;
+  // the null-stream copies below are not ordered with the caller's
+  // non-blocking streams: let a producer still writing the buffer finish
+  // first, so the saved bytes are the ones the restore must put back
+  hip_check(hipDeviceSynchronize(), "probe: drain the device");
   hip_check(hipMemcpy(&saved, p, e.probe, hipMemcpyDeviceToHost), "probe save");
   counter = counter * 6364136223846793005ull + 1442695040888963407ull + (uint64_t)myid;
   e.nonce = counter ^ saved;  // never the current contents
@@ -506,6 +579,7 @@ inline char *ipc_import(int peer, const IpcExport &e, std::vector<IpcKey> &held)
       it = m.emplace(k, IpcMapping{rit->ptr, 0, rit->bytes}).first;
       ipc_retired_bytes() -= rit->bytes;
       r.erase(rit);
+      ipc_live_bytes() += it->second.bytes;
     } else {
       void *ptr = nullptr;
       hip_check(hipIpcOpenMemHandle(&ptr, e.handle, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
@@ -516,7 +590,9 @@ inline char *ipc_import(int peer, const IpcExport &e, std::vector<IpcKey> &held)
         bytes = 0;
       }
       it = m.emplace(k, IpcMapping{(char *)ptr, 0, bytes}).first;
+      ipc_live_bytes() += bytes;
     }
+    ipc_live_peak() = std::max(ipc_live_peak(), ipc_live_bytes());
   }
   it->second.refs++;
   held.push_back(k);
@@ -538,6 +614,7 @@ inline void ipc_release(std::vector<IpcKey> &held) {
                  (void *)it->second.ptr);
       ipc_retired().push_back(IpcRetired{k, it->second.ptr, it->second.bytes});
       ipc_retired_bytes() += it->second.bytes;
+      ipc_live_bytes() -= it->second.bytes;
       m.erase(it);
     }
   }

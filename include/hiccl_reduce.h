@@ -201,6 +201,11 @@ int hiccl_reduce_plan_enqueue(hiccl_reduce_plan_t *plan, void *stream);
  * each one a one-shot hiccl_reduce_ex with the plan's configuration (AUTO
  * decides per compute). */
 int hiccl_reduce_plan_launch_each(hiccl_reduce_plan_t *plan, void *stream);
+/* Waits for the last hiccl_reduce_plan_launch (hipStreamSynchronize of its
+ * stream, compute.h:107-117).  After it returns the plan no longer refers to
+ * that stream: the caller may destroy the stream.  A plan destroyed or
+ * re-uploaded while a launch was never synchronised synchronises the launch's
+ * stream, which must then still exist. */
 int hiccl_reduce_plan_sync(hiccl_reduce_plan_t *plan);
 /* The plan's own non-blocking stream (a hipStream_t), created on the first
  * call and destroyed with the plan; NULL on error. */

@@ -137,3 +137,46 @@ def test_serial_rw_model():
     assert abs(m["predicted_ms"] - t * 1e3) < 1e-3 and abs(m["frac"] - 1.0) < 1e-3
     assert bench.serial_rw_model(r, w, None, copy, t) is None
     assert bench.serial_rw_model(r, w, read, 2 * read, t) is None  # copy faster than reads: no model
+
+
+def test_c5_child_env_drops_device_masks(monkeypatch):
+    """The config-5 MPI job picks each rank's GPU by local rank: a device mask
+    inherited from the torchrun rank (one GPU visible per process) would put
+    every MPI rank on that one GPU.  run_c5 drops the masks from the job's
+    environment, counts GPUs without them, and records what it dropped --
+    here (no GPU) in the skip record."""
+    import argparse
+    sys.path.insert(0, ROOT)
+    import bench
+    env = {"HIP_VISIBLE_DEVICES": "3", "ROCR_VISIBLE_DEVICES": "0", "CUDA_VISIBLE_DEVICES": "1", "KEEP": "x"}
+    child, dropped = bench.c5_child_env(env)
+    assert child == {"KEEP": "x"}
+    assert dropped == {"HIP_VISIBLE_DEVICES": "3", "ROCR_VISIBLE_DEVICES": "0", "CUDA_VISIBLE_DEVICES": "1"}
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5")
+    res = bench.run_c5(2, argparse.Namespace(c5_log2count=10, c5_iters=1))
+    assert res["env_scrubbed"] == {"HIP_VISIBLE_DEVICES": "5"}
+    assert res["devices_counted_unmasked"] == 0 and "one GPU per rank" in res["skipped"]
+
+
+def test_c5_driver_json_records_devices_and_mode(tmp_path):
+    """The C5 driver's JSON (HICCL_DRIVER_JSON; the same writer in the HIP
+    build bench.py runs) carries every rank's visible device count, device,
+    PCI bus id and the execution mode actually used, and parses as JSON --
+    exercised here on the host port (2 MPI ranks, no GPU)."""
+    import json
+    import shutil
+    import subprocess
+    mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
+    if not os.path.exists(mpirun):
+        pytest.skip("no mpirun")
+    subprocess.run(["make", "-C", ROOT, "build/collectives_host_f32"], check=True, stdout=subprocess.DEVNULL)
+    path = tmp_path / "c5.json"
+    env = dict(os.environ, OMP_NUM_THREADS="1", HICCL_DRIVER_JSON=str(path))
+    p = subprocess.run([mpirun, "-np", "2", os.path.join(ROOT, "build", "collectives_host_f32"), "8", "4096", "1", "1",
+                        "4", "1", "2", "2", "mpi"], capture_output=True, text=True, env=env, timeout=240, cwd="/tmp")
+    assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
+    r = json.loads(path.read_text())
+    assert r["kat"] == "PASSED" and r["ranks"] == 2
+    assert r["devices_seen"] == [0, 0] and r["rank_devices"] == [-1, -1]
+    assert r["bus_ids"] == ["host", "host"]
+    assert r["mode_used"] == "host-driven"

@@ -185,14 +185,18 @@ def test_shared_device_falls_back_to_host_driven(pattern):
     assert "ranks share a GPU" in out and "host-driven" in out
 
 
-def test_xccl_level_shared_device_uses_ipc_path():
-    """An XCCL level with ranks sharing the one GPU: RCCL refuses two ranks on
-    one device, so the level runs on the IPC path (said at init) and the
-    known-answer test passes."""
-    rc, out = mpirun(4, HIP, [8, 4099, 1, 1, 3, 0, 0, "2,2", "ipc,xccl"], streamed=False)
+@pytest.mark.parametrize("optin", [False, True], ids=["default", "rccl_requested"])
+def test_xccl_level_shared_device_uses_ipc_path(optin):
+    """An XCCL level runs on the (tested) IPC path unless HICCL_XCCL=rccl asks
+    for RCCL; asked, with ranks sharing the one GPU, RCCL refuses two ranks on
+    one device, so the level still runs on the IPC path.  Either way init says
+    why and the known-answer test passes."""
+    rc, out = mpirun(4, HIP, [8, 4099, 1, 1, 3, 0, 0, "2,2", "ipc,xccl"], streamed=False,
+                     extra_env={"HICCL_XCCL": "rccl"} if optin else None)
     assert rc == 0, out[-3000:]
     assert "PASSED!" in out
     assert "XCCL levels run on the IPC path" in out
+    assert ("ranks share a GPU" if optin else "RCCL is opt-in") in out
 
 
 def _ngpus():
@@ -206,6 +210,6 @@ def test_xccl_level_on_rccl(streamed):
     """One GPU per rank: the XCCL level moves its bytes with ncclSend/ncclRecv."""
     n = min(_ngpus(), 8)
     rc, out = mpirun(n, HIP, [8, 4099, 1, 1, 3, 0, 0, str(n), "xccl"], streamed=streamed,
-                     stream_env="1" if streamed else "0")
+                     stream_env="1" if streamed else "0", extra_env={"HICCL_XCCL": "rccl"})
     assert rc == 0, out[-3000:]
     assert "PASSED!" in out and "XCCL on RCCL" in out

@@ -457,6 +457,30 @@ def test_auto_wide_tiles_large_few_inputs(oracle, dtype, n):
     assert torch.equal(iv(outs["auto"][idx.to(DEV)].cpu()), iv(acc))
 
 
+@pytest.mark.parametrize("config", [dict(block=512), dict(nontemporal=1), dict(store_policy=1),
+                                    dict(block=256, nontemporal=1)],
+                         ids=["block512", "nt_off", "store_plain", "block256_nt_off"])
+def test_wide_tile_size_with_caller_shape_runs(oracle, config):
+    """1 GiB per input x 2 inputs is where AUTO picks wide tiles (U = 16), a
+    shape that exists only at block 256 with nt loads and stores.  A caller
+    asking for another block or cache policy at that size must still run
+    (u4 / PHASE, not 'unsupported config'), bit-exact vs the default call."""
+    count = 1 << 28
+    a = torch.empty(count, device=DEV)
+    b = torch.empty(count, device=DEV)
+    hiccl_amd.fill_uniform(a, 91, 0)
+    hiccl_amd.fill_uniform(b, 91, 1)
+    ref = torch.empty(count, device=DEV)
+    hiccl_amd.reduce(ref, [a, b])
+    out = torch.empty(count, device=DEV)
+    hiccl_amd.reduce(out, [a, b], config=config)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+    idx = torch.tensor([0, 1, count // 2, count - 1], device=DEV)
+    exp = ((torch.zeros(4, device=DEV) + a[idx]) + b[idx])
+    assert torch.equal(out[idx].view(torch.int32), exp.view(torch.int32))
+
+
 def test_plan_auto_engine_bf16():
     """bf16 with >= 5 inputs: AUTO takes TILE only from 64 tickets per
     workgroup (n = 8: 2^27 elements per input on 256 CUs), PHASE below;
