@@ -43,6 +43,7 @@ DTYPE_OF_TORCH = {
     torch.int64: HICCL_UINT64,  # two's-complement add == size_t add bit for bit
     torch.uint64: HICCL_UINT64,
     torch.int32: HICCL_INT32,
+    torch.uint8: HICCL_BYTES,  # exact byte copies (one input)
 }
 
 
@@ -102,6 +103,13 @@ _SIGS = {
                                              ctypes.c_double, _vp]),
     "hiccl_counter_add": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp]),
     "hiccl_signal_wait_phases": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, ctypes.c_double, _vp]),
+    "hiccl_program_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
+    "hiccl_program_add_signal": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp, ctypes.c_int]),
+    "hiccl_program_add_plan": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
+    "hiccl_program_num_segments": (ctypes.c_int, [_vp]),
+    "hiccl_program_num_phases": (ctypes.c_int, [_vp]),
+    "hiccl_program_launch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_double, _vp]),
+    "hiccl_program_destroy": (None, [_vp]),
 }
 
 

@@ -239,6 +239,61 @@ class Compute:
             pass
 
 
+class Program:
+    """A step program (include/hiccl_reduce.h ``hiccl_program_*``): an ordered
+    list of signal/wait phases and plans' computes that runs as ONE kernel
+    launch, each element after the previous one completed -- the ordered work
+    of one stream-ordered pipeline step (what HiCCL::Comm records per step).
+
+    add_signal(sig_ptrs, wait_ptrs)   one phase (device flag addresses).
+    add_plan(compute, join=False)     the computes a :class:`Compute` holds now
+                                      (its dtype must be the program's, or
+                                      torch.uint8 = exact byte copies).
+    launch(epochs, epoch_dev, err, timeout_s, stream)
+    """
+
+    def __init__(self, dtype=torch.float32, device=None):
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = device
+        h = ctypes.c_void_p()
+        L.check(L.lib().hiccl_program_create(ctypes.byref(h), L.DTYPE_OF_TORCH[dtype], device), "program_create")
+        self._prog = h
+        self._keep = []
+
+    def add_signal(self, sig_ptrs, wait_ptrs):
+        st, wt = _ptr_table(list(sig_ptrs)), _ptr_table(list(wait_ptrs))
+        L.check(L.lib().hiccl_program_add_signal(self._prog, st, len(sig_ptrs), wt, len(wait_ptrs)),
+                "program_add_signal")
+
+    def add_plan(self, compute, join=False):
+        L.check(L.lib().hiccl_program_add_plan(self._prog, compute._plan, 1 if join else 0), "program_add_plan")
+        self._keep.append(compute)
+
+    def segments(self):
+        return L.lib().hiccl_program_num_segments(self._prog)
+
+    def phases(self):
+        return L.lib().hiccl_program_num_phases(self._prog)
+
+    def launch(self, epochs=(), epoch_dev=None, err=None, timeout_s=10.0, stream=None):
+        ep = (ctypes.c_uint32 * max(1, len(epochs)))(*epochs)
+        L.check(L.lib().hiccl_program_launch(self._prog, ep, ctypes.c_void_p(epoch_dev or 0),
+                                             ctypes.c_void_p(err or 0), float(timeout_s),
+                                             _stream_handle(stream, self.device)), "program_launch")
+
+    def close(self):
+        if self._prog:
+            L.lib().hiccl_program_destroy(self._prog)
+            self._prog = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class HostPipe:
     """Host-resident buckets (include/hiccl_reduce.h hiccl_host_pipe_*):
     ``reduce(out, inputs)`` sums host tensors in list order on the GPU,

@@ -156,6 +156,7 @@ static int bench_json(const char *path, HiCCL::Comm<Type> &coll, Type *sendbuf_d
     if (coll.fused_gather()) mode_used += "+fused";
 #ifndef HICCL_PORT_HOST
     if (coll.xccl_on_rccl()) mode_used += "+xccl-rccl";
+    if (coll.step_program_mode()) mode_used += "+program";
     if (coll.shares_device()) mode_used += " (ranks share a GPU)";
 #endif
     std::string h, l;

@@ -736,6 +736,194 @@ __global__ __launch_bounds__(64) void k_counter_add(uint32_t *ctr, uint32_t v) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ------------------------------------------------------------ step programs --
+//
+// A stream-ordered pipeline step is a short ordered list of work: signal /
+// wait phases (ready tokens), the transport's batched copies, more phases
+// (done tokens), the step's reductions, the fused transfers' done tokens.
+// Launched one by one that is four or five kernels per step, each boundary
+// ~1.5-1.9 us (MI355X_MICROARCH.md).  A step PROGRAM runs the whole list in
+// one launch: the list is a sequence of SEGMENTS (kind 1: signal/wait phases,
+// run by one wave as k_sigwait_phases does; kind 0: units -- tiles of a set of
+// computes, reductions in the program's type or exact byte copies), and the
+// grid works through TICKETS taken in order from a device counter.  Ticket k
+// belongs to segment s(k); before working on it a workgroup waits until
+// segment s(k) - 1 is complete.  Every ticket of an earlier segment was taken
+// before k by a workgroup that is running, so the wait always ends: unlike a
+// grid barrier this needs no co-residency of the grid.  Completions are
+// published once per workgroup and segment (release fence at system scope --
+// peers read what the copies and reductions wrote -- then an agent-scope
+// counter add); a workgroup that passes a gate takes a system-scope acquire,
+// so the peers' writes its signal/wait segment waited for are seen by every
+// XCD's L2.  Same stores and waits, in the same order, as the separate
+// launches; bits identical.
+
+constexpr int kProgMaxSegs = 48;
+constexpr int kProgMaxPhases = 64;
+constexpr int kProgBlock = 256;
+constexpr int kProgPol = 11;  // nt loads, nt stores (the library's default policy)
+
+struct ProgSeg {
+  uint32_t tick_begin;  // first ticket (segment s owns [tick_begin, seg[s+1].tick_begin))
+  uint32_t kind;        // 0: units, 1: signal/wait phases
+  uint32_t first;       // units: first unit; phases: first phase
+  uint32_t count;       // units: units; phases: phases
+  uint32_t grab;        // units per ticket (units segments)
+  uint32_t need;        // completions that close the segment (its units, or 1)
+};
+
+struct ProgPhase {
+  uint32_t sig_begin, sig_end, wait_begin, wait_end;
+};
+
+struct ProgArgs {
+  const PlanDesc *desc;  // computes of every units segment; pad bit 0: exact byte copy
+  const char *const *ptrs;
+  const uint32_t *unit_comp;
+  const ProgPhase *phase;
+  uint32_t *const *sig;
+  const uint32_t *const *wait;
+  uint32_t *ctr;  // [0] tickets, [1] exits, [2 + s] completions of segment s; zero between launches
+  uint32_t *err;
+  const uint32_t *epoch_dev;
+  uint64_t timeout_ticks;
+  uint32_t stride, nseg, nticket, nphase;
+  ProgSeg seg[kProgMaxSegs];
+  uint32_t epoch[kProgMaxPhases];  // per launch: phase p stores / awaits epoch[p] (+ *epoch_dev)
+};
+
+// Bounded spin of one lane until *c >= need: false on time-out or an error
+// recorded by anyone (then *err is set and the caller goes on without
+// waiting, so the grid always drains).
+__device__ __forceinline__ void prog_gate_wait(const ProgArgs &a, const uint32_t *c, uint32_t need) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need) {
+    __builtin_amdgcn_s_sleep(1);
+    if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+      if (a.err) __hip_atomic_store(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
+}
+
+// Phases [first, first + count) on one wave (lanes = flags), as k_sigwait_phases.
+__device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t first, uint32_t count, uint32_t lane,
+                                            uint32_t add) {
+  for (uint32_t p = first; p < first + count; p++) {
+    const ConstU32 *q = (const ConstU32 *)&a.phase[p];
+    const uint32_t s0 = q[0], s1 = q[1], w0 = q[2], w1 = q[3];
+    const uint32_t epoch = a.epoch[p] + add;
+    for (uint32_t i = s0 + lane; i < s1; i += 64)
+      __hip_atomic_store(((uint32_t *const __attribute__((address_space(4))) *)a.sig)[i], epoch, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint32_t i = w0 + lane; i < w1; i += 64) {
+      const uint32_t *f = ((const uint32_t *const __attribute__((address_space(4))) *)a.wait)[i];
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((int32_t)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+          if (a.err) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+    }
+    // every lane's waits of this phase precede any store of the next one
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+  }
+}
+
+template <class Op, int U>
+__device__ __forceinline__ void prog_unit_of(const PlanDesc &d, TableInputs raw, uint64_t lt, int tid,
+                                             const uint32_t (&voff)[U]) {
+  constexpr uint64_t TILE = (uint64_t)kProgBlock * U;
+  if (lt == 0) scalar_part<Op>(d.out, raw, d.n, d.head, d.npkt, d.tail, tid);
+  const uint64_t pkt0 = lt * TILE;
+  if (pkt0 >= d.npkt) return;
+  const uint64_t shift = (uint64_t)d.head * Op::kEsz;
+  Shifted<TableInputs> in{raw, shift};
+  const uint64_t left = d.npkt - pkt0;
+  const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
+  tile_body<Op, U, kProgPol>(d.out + shift, in, d.n, pkt0 * kPacket, tile_bytes, voff);
+}
+
+template <class Op, int U>
+__global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
+  const int tid = threadIdx.x;
+  uint32_t voff[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * kProgBlock + tid) * kPacket);
+  __shared__ uint32_t s_tick[2];
+  const uint32_t add = a.epoch_dev ? __hip_atomic_load(a.epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  if (tid == 0) s_tick[0] = __hip_atomic_fetch_add(&a.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  uint32_t k = __builtin_amdgcn_readfirstlane(s_tick[0]);  // workgroup-uniform: scalar from here on
+  int slot = 0;
+  uint32_t open = 0;               // segments below `open` are complete, as this workgroup has seen
+  uint32_t pend_seg = 0, pend = 0;  // completions of pend_seg done here, not yet published
+  auto publish = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this wave's stores done and written back (system scope)
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&a.ctr[2 + pend_seg], pend, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    pend = 0;
+  };
+  while (k < a.nticket) {
+    uint32_t s = 0;  // the segment of ticket k (kernarg: scalar loads)
+    while (s + 1 < a.nseg && a.seg[s + 1].tick_begin <= k) s++;
+    // the next ticket, taken before this one's work (its latency hides under it)
+    uint32_t nxt = 0;
+    if (tid == 0) nxt = __hip_atomic_fetch_add(&a.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (pend && pend_seg != s) publish();  // before any wait: others may be waiting for it
+    if (s > open) {
+      if (tid == 0) prog_gate_wait(a, &a.ctr[2 + s - 1], a.seg[s - 1].need);
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // see what the completed segments (and peers) wrote
+      open = s;
+    }
+    const uint32_t kind = a.seg[s].kind, first = a.seg[s].first, count = a.seg[s].count;
+    if (kind == 1) {
+      if (tid < 64) prog_phases(a, first, count, (uint32_t)tid, add);
+      pend_seg = s;
+      pend = 1;
+    } else {
+      const uint32_t grab = a.seg[s].grab;
+      const uint32_t u0 = first + (k - a.seg[s].tick_begin) * grab;
+      const uint32_t u1 = u0 + grab < first + count ? u0 + grab : first + count;
+      for (uint32_t t = u0; t < u1; t++) {
+        const uint32_t c = a.unit_comp ? ((ConstU32 *)a.unit_comp)[t] : 0u;
+        const ConstDesc *q = (const ConstDesc *)a.desc + c;
+        const PlanDesc d = load_desc(a.desc, c);
+        const bool bytes = (q->pad & 1u) != 0;
+        TableInputs raw{a.ptrs + (uint64_t)c * a.stride};
+        if (bytes)
+          prog_unit_of<OpRaw, U>(d, raw, t - d.tile_begin, tid, voff);
+        else
+          prog_unit_of<Op, U>(d, raw, t - d.tile_begin, tid, voff);
+      }
+      pend_seg = s;
+      pend += u1 - u0;
+    }
+    if (tid == 0) s_tick[slot ^ 1] = nxt;
+    __syncthreads();
+    slot ^= 1;
+    k = __builtin_amdgcn_readfirstlane(s_tick[slot]);
+  }
+  if (pend) publish();
+  if (tid == 0) {
+    // every ticket take of this workgroup precedes its exit increment; the
+    // last one out leaves the counters zero for the next launch
+    const uint32_t prev = __hip_atomic_fetch_add(&a.ctr[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(&a.ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.ctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t s = 0; s < a.nseg; s++)
+        __hip_atomic_store(&a.ctr[2 + s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // ------------------------------------------------------------ host side ----
 
 struct DevInfo {
@@ -1887,6 +2075,294 @@ int hiccl_signal_wait_phases(const hiccl_signal_phase_t *ph, int nph, const uint
         return e;
   }
   return launch();
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ step programs --
+
+struct hiccl_program {
+  int dtype = 0;
+  int device = 0;
+  struct Unit {
+    void *out;
+    std::vector<const void *> in;
+    size_t count;
+    bool bytes;  // exact byte copy (a HICCL_BYTES plan's compute)
+  };
+  struct Seg {
+    int kind;  // 0 units, 1 signal/wait phases
+    std::vector<Unit> units;
+    uint32_t phase0, nphase;
+  };
+  std::vector<Seg> segs;
+  struct Phase {
+    std::vector<uint32_t *> sig;
+    std::vector<const uint32_t *> wait;
+  };
+  std::vector<Phase> phases;
+  bool dirty = true;
+  char *d_block = nullptr;
+  uint32_t *d_ctr = nullptr;
+  ProgArgs args;
+  int unroll = 4;
+  uint32_t grid = 0;
+  std::atomic<bool> enqueued{false};
+};
+
+namespace {
+
+constexpr int kProgBpc = 2;           // workgroups per CU of a program launch
+constexpr uint32_t kProgTicketsPerWG = 16;  // units segments: about this many tickets per workgroup at most
+
+typedef void (*prog_fn)(const ProgArgs &, dim3, hipStream_t);
+
+template <class Op, int U>
+void launch_prog_t(const ProgArgs &a, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((k_program<Op, U>), grid, dim3(kProgBlock), 0, s, a);
+}
+
+prog_fn pick_prog(int dtype, int unroll) {
+  const bool u2 = unroll == 2;
+  switch (dtype) {
+    case HICCL_FLOAT32: return u2 ? launch_prog_t<OpF32, 2> : launch_prog_t<OpF32, 4>;
+    case HICCL_BFLOAT16: return u2 ? launch_prog_t<OpBF16, 2> : launch_prog_t<OpBF16, 4>;
+    case HICCL_FLOAT64: return u2 ? nullptr : launch_prog_t<OpF64, 4>;
+    case HICCL_UINT64: return u2 ? nullptr : launch_prog_t<OpU64, 4>;
+    case HICCL_INT32: return u2 ? nullptr : launch_prog_t<OpI32, 4>;
+    case HICCL_BYTES: return u2 ? nullptr : launch_prog_t<OpRaw, 4>;
+    default: return nullptr;
+  }
+}
+
+void prog_quiesce(hiccl_program *p) {
+  if (p->enqueued.load(std::memory_order_relaxed)) {
+    (void)hipDeviceSynchronize();
+    p->enqueued.store(false, std::memory_order_relaxed);
+  }
+}
+
+int prog_upload(hiccl_program *p, hipStream_t s) {
+  if (!p->dirty) return 0;
+  if (capturing(s, false))
+    return fail(hipErrorStreamCaptureUnsupported,
+                "program: the first launch after a change uploads the program and cannot be captured");
+  prog_quiesce(p);
+  if (p->d_block) {
+    (void)hipFree(p->d_block);
+    p->d_block = nullptr;
+  }
+  if (!p->d_ctr) {
+    if (int e = check_hip(hipMalloc((void **)&p->d_ctr, 256), "program: hipMalloc(counters)")) return e;
+    if (int e = check_hip(hipMemset(p->d_ctr, 0, 256), "program: hipMemset(counters)")) return e;
+  }
+  const int cus = device_cus(p->device);
+  const size_t tesz = esize(p->dtype);
+  auto esz_of = [&](const hiccl_program::Unit &u) { return u.bytes ? (size_t)1 : tesz; };
+  // one tile shape for the launch: half-size tiles when the whole program
+  // has under two 16 KiB tiles per CU (auto_unroll; the C5 step)
+  uint64_t total_pkt = 0;
+  size_t ncomp = 0, maxn = 1;
+  for (auto &g : p->segs)
+    for (auto &u : g.units) {
+      total_pkt += split_on(u.out, u.count, esz_of(u)).npkt;
+      ncomp++;
+      if (u.in.size() > maxn) maxn = u.in.size();
+    }
+  p->unroll = pick_prog(p->dtype, 2) && total_pkt < 2ull * cus * kProgBlock * 4 ? 2 : 4;
+  const uint64_t unit = (uint64_t)kProgBlock * p->unroll;
+  // the units of every segment, in order, and the ticket layout
+  const uint32_t grid_cap = (uint32_t)(cus * kProgBpc);
+  std::vector<uint32_t> unit_comp;
+  std::vector<PlanDesc> desc(ncomp);
+  std::vector<const void *> ptrs(ncomp * maxn, nullptr);
+  ProgArgs &a = p->args;
+  memset(&a, 0, sizeof(a));
+  uint64_t tickets = 0;
+  size_t c = 0;
+  for (size_t si = 0; si < p->segs.size(); si++) {
+    auto &g = p->segs[si];
+    ProgSeg &ps = a.seg[si];
+    ps.tick_begin = (uint32_t)tickets;
+    ps.kind = (uint32_t)g.kind;
+    if (g.kind == 1) {
+      ps.first = g.phase0;
+      ps.count = g.nphase;
+      ps.grab = 1;
+      ps.need = 1;
+      tickets += 1;
+      continue;
+    }
+    ps.first = (uint32_t)unit_comp.size();
+    for (auto &u : g.units) {
+      const Split sp = split_on(u.out, u.count, esz_of(u));
+      PlanDesc &d = desc[c];
+      d.out = (char *)u.out;
+      d.npkt = sp.npkt;
+      d.head = sp.head;
+      d.tail = sp.tail;
+      d.n = (uint32_t)u.in.size();
+      d.pad = u.bytes ? 1u : 0u;
+      d.tile_begin = unit_comp.size();
+      for (size_t k = 0; k < u.in.size(); k++) ptrs[c * maxn + k] = u.in[k];
+      const uint64_t nt = tiles_for(sp.npkt, unit);
+      for (uint64_t t = 0; t < nt; t++) unit_comp.push_back((uint32_t)c);
+      c++;
+    }
+    const uint64_t units = unit_comp.size() - ps.first;
+    if (units > 0xffffffffull || unit_comp.size() > 0xffffffffull)
+      return fail(hipErrorInvalidValue, "program: more than 2^32 tiles");
+    ps.count = (uint32_t)units;
+    const uint64_t per = (uint64_t)grid_cap * kProgTicketsPerWG;
+    ps.grab = (uint32_t)(units > per ? (units + per - 1) / per : 1);
+    ps.need = (uint32_t)units;
+    tickets += (units + ps.grab - 1) / ps.grab;
+  }
+  if (tickets > 0xffffffffull) return fail(hipErrorInvalidValue, "program: too many tickets");
+  a.nseg = (uint32_t)p->segs.size();
+  a.nticket = (uint32_t)tickets;
+  a.nphase = (uint32_t)p->phases.size();
+  a.stride = (uint32_t)maxn;
+  p->grid = (uint32_t)(tickets < grid_cap ? tickets : grid_cap);
+  // device block: [desc | ptrs | unit_comp | phases | sig | wait]
+  size_t nsig = 0, nwait = 0;
+  for (auto &ph : p->phases) {
+    nsig += ph.sig.size();
+    nwait += ph.wait.size();
+  }
+  auto al8 = [](size_t x) { return (x + 7) & ~(size_t)7; };
+  const size_t o_desc = 0, o_ptrs = al8(o_desc + ncomp * sizeof(PlanDesc));
+  const size_t o_uc = al8(o_ptrs + ptrs.size() * sizeof(void *));
+  const size_t o_ph = al8(o_uc + unit_comp.size() * sizeof(uint32_t));
+  const size_t o_sig = al8(o_ph + p->phases.size() * sizeof(ProgPhase));
+  const size_t o_wait = al8(o_sig + nsig * sizeof(void *));
+  const size_t bytes = al8(o_wait + nwait * sizeof(void *)) + 8;
+  std::vector<char> host(bytes, 0);
+  if (ncomp) memcpy(host.data() + o_desc, desc.data(), ncomp * sizeof(PlanDesc));
+  if (!ptrs.empty()) memcpy(host.data() + o_ptrs, ptrs.data(), ptrs.size() * sizeof(void *));
+  if (!unit_comp.empty()) memcpy(host.data() + o_uc, unit_comp.data(), unit_comp.size() * sizeof(uint32_t));
+  {
+    ProgPhase *hp = (ProgPhase *)(host.data() + o_ph);
+    uint32_t **hs = (uint32_t **)(host.data() + o_sig);
+    const uint32_t **hw = (const uint32_t **)(host.data() + o_wait);
+    uint32_t si = 0, wi = 0;
+    for (size_t i = 0; i < p->phases.size(); i++) {
+      auto &ph = p->phases[i];
+      hp[i].sig_begin = si;
+      for (auto *f : ph.sig) hs[si++] = f;
+      hp[i].sig_end = si;
+      hp[i].wait_begin = wi;
+      for (auto *f : ph.wait) hw[wi++] = f;
+      hp[i].wait_end = wi;
+    }
+  }
+  if (int e = check_hip(hipMalloc((void **)&p->d_block, bytes), "program: hipMalloc")) return e;
+  if (int e = check_hip(hipMemcpy(p->d_block, host.data(), bytes, hipMemcpyHostToDevice), "program: upload"))
+    return e;
+  a.desc = (const PlanDesc *)(p->d_block + o_desc);
+  a.ptrs = (const char *const *)(p->d_block + o_ptrs);
+  a.unit_comp = (const uint32_t *)(p->d_block + o_uc);
+  a.phase = (const ProgPhase *)(p->d_block + o_ph);
+  a.sig = (uint32_t *const *)(p->d_block + o_sig);
+  a.wait = (const uint32_t *const *)(p->d_block + o_wait);
+  a.ctr = p->d_ctr;
+  p->dirty = false;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hiccl_program_create(hiccl_program_t **prog, int dtype, int device) {
+  if (!prog) return fail(hipErrorInvalidValue, "program_create: prog is NULL");
+  *prog = nullptr;
+  if (!pick_prog(dtype, 4)) return fail(hipErrorInvalidValue, "program_create: unsupported dtype");
+  int ndev = 0;
+  if (int e = check_hip(hipGetDeviceCount(&ndev), "program_create: hipGetDeviceCount")) return e;
+  if (device < 0 || device >= ndev) return fail(hipErrorInvalidDevice, "program_create: bad device");
+  auto *p = new hiccl_program;
+  p->dtype = dtype;
+  p->device = device;
+  *prog = p;
+  return 0;
+}
+
+int hiccl_program_add_signal(hiccl_program_t *p, uint32_t *const *sig, int nsig, const uint32_t *const *wait,
+                             int nwait) {
+  if (!p) return fail(hipErrorInvalidValue, "program_add_signal: prog is NULL");
+  if (nsig < 0 || nwait < 0 || (nsig && !sig) || (nwait && !wait))
+    return fail(hipErrorInvalidValue, "program_add_signal: bad flag lists");
+  for (int i = 0; i < nsig; i++)
+    if (!sig[i]) return fail(hipErrorInvalidValue, "program_add_signal: NULL signal flag");
+  for (int i = 0; i < nwait; i++)
+    if (!wait[i]) return fail(hipErrorInvalidValue, "program_add_signal: NULL wait flag");
+  if (p->phases.size() >= (size_t)kProgMaxPhases)
+    return fail(hipErrorInvalidValue, "program_add_signal: more than 64 phases in one program");
+  // consecutive phases share one segment (one wave runs them in order)
+  if (p->segs.empty() || p->segs.back().kind != 1) {
+    if (p->segs.size() >= (size_t)kProgMaxSegs)
+      return fail(hipErrorInvalidValue, "program_add_signal: more than 48 segments in one program");
+    p->segs.push_back(hiccl_program::Seg{1, {}, (uint32_t)p->phases.size(), 0});
+  }
+  hiccl_program::Phase ph;
+  ph.sig.assign(sig, sig + nsig);
+  ph.wait.assign(wait, wait + nwait);
+  p->phases.push_back(std::move(ph));
+  p->segs.back().nphase++;
+  p->dirty = true;
+  return 0;
+}
+
+int hiccl_program_add_plan(hiccl_program_t *p, const hiccl_reduce_plan_t *plan, int join) {
+  if (!p || !plan) return fail(hipErrorInvalidValue, "program_add_plan: NULL argument");
+  const bool bytes = plan->dtype == HICCL_BYTES;
+  if (!bytes && plan->dtype != p->dtype)
+    return fail(hipErrorInvalidValue, "program_add_plan: the plan's dtype is neither the program's nor HICCL_BYTES");
+  if (plan->req.acc == HICCL_ACC_WIDE)
+    return fail(hipErrorInvalidValue, "program_add_plan: programs accumulate natively (HICCL_ACC_NATIVE) only");
+  if (plan->comps.empty()) return 0;
+  if (!join || p->segs.empty() || p->segs.back().kind != 0) {
+    if (p->segs.size() >= (size_t)kProgMaxSegs)
+      return fail(hipErrorInvalidValue, "program_add_plan: more than 48 segments in one program");
+    p->segs.push_back(hiccl_program::Seg{0, {}, 0, 0});
+  }
+  for (auto &c : plan->comps) p->segs.back().units.push_back(hiccl_program::Unit{c.out, c.in, c.count, bytes});
+  p->dirty = true;
+  return 0;
+}
+
+int hiccl_program_num_segments(const hiccl_program_t *p) { return p ? (int)p->segs.size() : 0; }
+int hiccl_program_num_phases(const hiccl_program_t *p) { return p ? (int)p->phases.size() : 0; }
+
+int hiccl_program_launch(hiccl_program_t *p, const uint32_t *epochs, const uint32_t *epoch_dev, uint32_t *err,
+                         double timeout_s, void *stream) {
+  if (!p) return fail(hipErrorInvalidValue, "program_launch: prog is NULL");
+  if (!p->phases.empty() && !epochs) return fail(hipErrorInvalidValue, "program_launch: epochs is NULL");
+  if (int e = check_hip(hipSetDevice(p->device), "program_launch: hipSetDevice")) return e;
+  if (p->segs.empty()) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (int e = prog_upload(p, s)) return e;
+  if (p->args.nticket == 0) return 0;
+  prog_fn fn = pick_prog(p->dtype, p->unroll);
+  if (!fn) return fail(hipErrorInvalidValue, "program_launch: no kernel for this dtype / shape");
+  ProgArgs a = p->args;
+  a.err = err;
+  a.epoch_dev = epoch_dev;
+  a.timeout_ticks = (uint64_t)((timeout_s > 0 ? timeout_s : 30.0) * 1e8);  // s_memrealtime: 100 MHz
+  for (uint32_t i = 0; i < a.nphase; i++) a.epoch[i] = epochs[i];
+  fn(a, dim3(p->grid), s);
+  p->enqueued.store(true, std::memory_order_relaxed);
+  return check_hip(hipGetLastError(), "program_launch: launch");
+}
+
+void hiccl_program_destroy(hiccl_program_t *p) {
+  if (!p) return;
+  (void)hipSetDevice(p->device);
+  prog_quiesce(p);
+  if (p->d_block) (void)hipFree(p->d_block);
+  if (p->d_ctr) (void)hipFree(p->d_ctr);
+  delete p;
 }
 
 // ---------------------------------------------------------- measurement --

@@ -255,6 +255,7 @@ class Comm {
     command_batch = instantiate(steps, libs, fused);
     CommBench::stream_ordered = false;
 #ifndef HICCL_PORT_HOST
+    programs = streamed && want_programs();
     if (streamed) {  // one flag pair per registered transfer, every rank the same layout
       size_t total = 0;
       for (auto &lst : command_batch)
@@ -277,6 +278,9 @@ class Comm {
       std::printf("initialization time: %e seconds (%zu steps, %zu libraries, %s%s%s%s)\n", MPI_Wtime() - t0,
                   steps.size(), libs.size(), streamed ? "stream-ordered" : "host-driven", graphed ? ", graph replay" : "",
                   fused ? ", fused gather" : "", xccl ? ", XCCL on RCCL" : "");
+#ifndef HICCL_PORT_HOST
+    if (programs && CommBench::myid == CommBench::printid) std::printf("step programs: one launch per step\n");
+#endif
   }
 
   bool xccl_on_rccl() const { return xccl; }
@@ -284,6 +288,9 @@ class Comm {
 
   bool stream_ordered() const { return streamed; }
   bool fused_gather() const { return fused; }
+#ifndef HICCL_PORT_HOST
+  bool step_program_mode() const { return programs; }
+#endif
 
   // ----------------------------------------------------------------- run --
   // comm.h:181-206
@@ -449,15 +456,71 @@ class Comm {
     const size_t nl = command_batch.size();
     std::vector<typename std::list<Command<T>>::iterator> it(nl);
     for (size_t i = 0; i < nl; i++) it[i] = command_batch[i].begin();
+    size_t step = 0;
     while (it[0] != command_batch[0].end()) {
-      for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
-      for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
-      for (size_t i = 0; i < nl; i++) {
-        it[i]->comm->enqueue_tail(s);
-        ++it[i];
+      if (programs) {
+        launch_step_program(step, it, s);
+      } else {
+        for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
+        for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
+        for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue_tail(s);
       }
+      for (size_t i = 0; i < nl; i++) ++it[i];
+      step++;
     }
     CommBench::flush_signals();  // (the last step's done tokens)
+  }
+
+  // Step programs (HICCL_STEP_PROGRAM, on by default in stream-ordered mode):
+  // each pipeline step -- every library's ready tokens, copies and done
+  // tokens, the computes in reverse library order, the fused transfers' done
+  // tokens, i.e. the enqueue order above -- is recorded once (the first
+  // eager run) into a hiccl_program and from then on runs as ONE kernel
+  // launch per step (hiccl_program_launch; reference: comm.h:195-204's
+  // transport wait -> compute start -> compute wait, one boundary per call).
+  // The phases' epochs are read from their transports at each launch.
+  struct StepProgram {
+    hiccl_program_t *prog = nullptr;
+    std::vector<std::function<uint32_t()>> epoch_of;
+  };
+  std::vector<StepProgram> step_programs;
+  bool programs = false;
+  bool in_capture = false;
+
+  template <class It>
+  void launch_step_program(size_t step, It &it, hipStream_t s) {
+    const size_t nl = command_batch.size();
+    if (step >= step_programs.size()) {  // record (never inside a capture: the first run is eager)
+      if (in_capture) CommBench::die("step program", "a step was first met inside a graph capture");
+      CommBench::flush_signals();
+      CommBench::StepRecorder rec;
+      if (hiccl_program_create(&rec.prog, dtype_of<T>(), CommBench::mydevice))
+        CommBench::die("step program", hiccl_last_error());
+      CommBench::step_recorder() = &rec;
+      for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
+      for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
+      for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue_tail(s);
+      CommBench::flush_signals();
+      CommBench::step_recorder() = nullptr;
+      step_programs.push_back(StepProgram{rec.prog, std::move(rec.epoch_of)});
+    } else {
+      for (size_t i = 0; i < nl; i++) it[i]->comm->advance();  // the execution counts, as enqueue() would
+    }
+    StepProgram &sp = step_programs[step];
+    std::vector<uint32_t> epochs(sp.epoch_of.size());
+    for (size_t i = 0; i < epochs.size(); i++) epochs[i] = sp.epoch_of[i]();
+    if (hiccl_program_launch(sp.prog, epochs.data(), in_capture ? graph_ctr : nullptr, flags.err, CommBench::signal_timeout(),
+                             s))
+      CommBench::die("step program", hiccl_last_error());
+  }
+
+  bool want_programs() {
+    const char *env = std::getenv("HICCL_STEP_PROGRAM");
+    int on = !(env && std::string(env) == "0");
+    for (auto &lst : command_batch)
+      for (auto &c : lst) on = on && c.comm->recordable();
+    MPI_Allreduce(MPI_IN_PLACE, &on, 1, MPI_INT, MPI_LAND, CommBench::comm_mpi);
+    return on != 0;
   }
 
   template <class F>
@@ -478,7 +541,9 @@ class Comm {
     CommBench::hip_check(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "graph: begin capture");
     if (hiccl_counter_add(graph_ctr, 1, s)) CommBench::die("graph: counter", hiccl_last_error());
     for_each_comm([this](CommBench::Comm<T> &c) { c.begin_capture(graph_ctr); });
+    in_capture = true;
     enqueue_pipeline(s);
+    in_capture = false;
     for_each_comm([](CommBench::Comm<T> &c) { c.end_capture(); });
     graph_base.clear();
     for_each_comm([this](CommBench::Comm<T> &c) { graph_base.push_back(c.epoch_now()); });
@@ -525,6 +590,8 @@ class Comm {
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph_ctr) (void)hipFree(graph_ctr);
     if (!owned.empty() || !command_batch.empty()) (void)hipDeviceSynchronize();
+    for (auto &sp : step_programs) hiccl_program_destroy(sp.prog);
+    step_programs.clear();
 #endif
     // the steps' transports (releasing their IPC mappings) and computes (the
     // reference never deletes them)

@@ -142,6 +142,7 @@ class Compute {
   void launch(hipStream_t s) {
     if (!numcomp) return;
     CommBench::flush_signals();  // queued signal/wait steps precede this kernel on the stream
+    if (CommBench::step_recorder()) return CommBench::record_plan(plan, 2, this);  // a step program's element
     check(hiccl_reduce_plan_enqueue(plan, s), "plan_enqueue");  // the caller syncs the stream
   }
 #endif

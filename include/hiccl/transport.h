@@ -42,6 +42,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -685,6 +686,7 @@ struct PendingSignals {
   struct Phase {
     std::vector<uint32_t *> sig, wait;
     uint32_t epoch;
+    std::function<uint32_t()> epoch_now;  // the owner's epoch for this phase at any later launch (step programs)
   };
   std::vector<Phase> phases;
   const uint32_t *epoch_dev = nullptr;
@@ -699,9 +701,50 @@ inline PendingSignals &pending_signals() {
   return p;
 }
 
+// Step programs (HiCCL::Comm, stream-ordered mode; hiccl_program_*): while a
+// recorder is set on this thread, flush_signals() and the transport's and
+// computes' plan launches APPEND to the recorder's program instead of
+// enqueueing -- the step's whole ordered work then goes out as one launch.
+// A phase's epoch is not fixed in the program: epoch_of[p]() gives it at
+// each launch (the owning transport's current epoch).
+struct StepRecorder {
+  hiccl_program_t *prog = nullptr;
+  std::vector<std::function<uint32_t()>> epoch_of;
+  int last = 0;                   // kind of the last element appended: 0 phases, 1 copies, 2 computes
+  const void *last_owner = nullptr;  // the transport whose copies were appended last
+};
+inline StepRecorder *&step_recorder() {
+  static thread_local StepRecorder *r = nullptr;
+  return r;
+}
+
+// Append plan `p` to the recording program: copies of one transport's
+// execution (move + self plans) share an element, so do the computes of a
+// step (the reference starts them together on separate streams,
+// comm.h:198-202, so they are independent); anything else starts after the
+// previous element.
+inline void record_plan(hiccl_reduce_plan_t *p, int kind, const void *owner) {
+  StepRecorder *r = step_recorder();
+  const bool join = r->last == kind && (kind == 2 || r->last_owner == owner);
+  if (hiccl_program_add_plan(r->prog, p, join ? 1 : 0)) die("step program", hiccl_last_error());
+  r->last = kind;
+  r->last_owner = owner;
+}
+
 inline void flush_signals() {
   PendingSignals &p = pending_signals();
   if (p.phases.empty()) return;
+  if (StepRecorder *r = step_recorder()) {
+    for (auto &ph : p.phases) {
+      if (hiccl_program_add_signal(r->prog, ph.sig.data(), (int)ph.sig.size(),
+                                   (const uint32_t *const *)ph.wait.data(), (int)ph.wait.size()))
+        die("step program", hiccl_last_error());
+      r->epoch_of.push_back(ph.epoch_now);
+    }
+    r->last = 0;
+    p.phases.clear();
+    return;
+  }
   std::vector<hiccl_signal_phase_t> ph(p.phases.size());
   for (size_t i = 0; i < ph.size(); i++) {
     ph[i].sig = p.phases[i].sig.data();
@@ -717,14 +760,15 @@ inline void flush_signals() {
 
 // epoch_dev != NULL (graph capture): the epoch used is epoch + *epoch_dev at run time.
 inline void signal_wait(const std::vector<uint32_t *> &sig, const std::vector<uint32_t *> &wait, uint32_t epoch,
-                        const uint32_t *epoch_dev, uint32_t *err, hipStream_t stream) {
+                        const uint32_t *epoch_dev, uint32_t *err, hipStream_t stream,
+                        std::function<uint32_t()> epoch_now = nullptr) {
   if (sig.empty() && wait.empty()) return;
   PendingSignals &p = pending_signals();
   if (!p.phases.empty() && (p.epoch_dev != epoch_dev || p.err != err || p.stream != stream)) flush_signals();
   p.epoch_dev = epoch_dev;
   p.err = err;
   p.stream = stream;
-  p.phases.push_back(PendingSignals::Phase{sig, wait, epoch});
+  p.phases.push_back(PendingSignals::Phase{sig, wait, epoch, std::move(epoch_now)});
 }
 #endif
 
@@ -896,11 +940,18 @@ class Comm {
       xccl_group(s);
       return;
     }
-    signal_wait(pre_sig, pre_wait, sig_epoch(), graph_epoch, flags->err, s);
+    signal_wait(pre_sig, pre_wait, sig_epoch(), graph_epoch, flags->err, s, epoch_fn());
     launch_copies(s);
-    signal_wait(post_sig, post_wait, sig_epoch(), graph_epoch, flags->err, s);
+    signal_wait(post_sig, post_wait, sig_epoch(), graph_epoch, flags->err, s, epoch_fn());
   }
-  void enqueue_tail(hipStream_t s) { signal_wait(tail_sig, tail_wait, sig_epoch(), graph_epoch, flags->err, s); }
+  void enqueue_tail(hipStream_t s) {
+    signal_wait(tail_sig, tail_wait, sig_epoch(), graph_epoch, flags->err, s, epoch_fn());
+  }
+  // A recorded step program runs instead of enqueue(): the execution still
+  // counts (the program's phases read sig_epoch() at each launch).
+  void advance() { ++epoch; }
+  // Can this transport's executions be recorded into a step program?
+  bool recordable() const { return lib != XCCL; }
 
   // hipGraph capture of stream-ordered executions (HiCCL::Comm::run with
   // HICCL_GRAPH=1): while `ctr` is set, every wait is enqueued as
@@ -1092,6 +1143,9 @@ class Comm {
   uint32_t epoch = 0;
   const uint32_t *graph_epoch = nullptr;  // set while a graph is being captured
   uint32_t sig_epoch() const { return graph_epoch ? epoch - 1 : epoch; }
+  std::function<uint32_t()> epoch_fn() const {
+    return [this] { return sig_epoch(); };
+  }
   std::vector<uint32_t *> pre_sig, pre_wait, post_sig, post_wait, tail_sig, tail_wait;
   // batched exact copies (HICCL_BYTES plans): the bytes this rank moves to or
   // from peers, and its self transfers -- one kernel each per execution
@@ -1121,8 +1175,9 @@ class Comm {
 
   // the transport synchronises its stream (or orders it by flags), never a
   // plan's completion event: enqueue without one
-  static void launch_plan(hiccl_reduce_plan_t *p, hipStream_t s, const char *what) {
+  void launch_plan(hiccl_reduce_plan_t *p, hipStream_t s, const char *what) {
     flush_signals();  // queued signal/wait steps precede this kernel on the stream
+    if (step_recorder()) return record_plan(p, 1, this);
     if (hiccl_reduce_plan_enqueue(p, s)) die(what, hiccl_last_error());
   }
 

@@ -285,6 +285,43 @@ int hiccl_signal_wait_phases(const hiccl_signal_phase_t *phases, int nphases, co
                              uint32_t *err, double timeout_s, void *stream);
 
 /* ----------------------------------------------------------------------
+ * Step programs: one launch per pipeline step (stream-ordered transport).
+ *
+ * The reference runs a step as transport start -> transport wait -> compute
+ * start -> compute wait (comm.h:195-204), i.e. separate launches and host
+ * synchronisations per step.  A program is the ordered work of one step --
+ * signal/wait phases (as hiccl_signal_wait_phases) and the computes of
+ * plans (reductions of the program's dtype, or HICCL_BYTES exact copies) --
+ * executed by ONE persistent kernel launch: each element runs after the
+ * previous one has completed (a device-side ticket order with per-element
+ * completion counters, no grid barrier), with the same stores, waits and
+ * results as launching them one by one on a stream.
+ *
+ * add_signal appends one phase (consecutive phases form one element, run
+ *   in order by one wave); its epoch is supplied per launch.
+ * add_plan appends the plan's computes as of this call (later adds to the
+ *   plan are not seen): join != 0 puts them in the same element as the
+ *   previous plan's (no ordering between them: independent outputs),
+ *   otherwise they start after it.  The plan's dtype must be the program's
+ *   or HICCL_BYTES; native accumulation only.
+ * launch: epochs[p] for every phase p (+ *epoch_dev when not NULL, read at
+ *   run time: graph replays), err / timeout_s as hiccl_signal_wait.  The
+ *   first launch (and the first after a change) uploads the program's tables
+ *   and cannot be captured into a graph.  One launch of a program at a time.
+ * Limits: 48 elements, 64 phases per program.
+ */
+typedef struct hiccl_program hiccl_program_t;
+int hiccl_program_create(hiccl_program_t **prog, int dtype, int device);
+int hiccl_program_add_signal(hiccl_program_t *prog, uint32_t *const *sig, int nsig, const uint32_t *const *wait,
+                             int nwait);
+int hiccl_program_add_plan(hiccl_program_t *prog, const hiccl_reduce_plan_t *plan, int join);
+int hiccl_program_num_segments(const hiccl_program_t *prog);
+int hiccl_program_num_phases(const hiccl_program_t *prog);
+int hiccl_program_launch(hiccl_program_t *prog, const uint32_t *epochs, const uint32_t *epoch_dev, uint32_t *err,
+                         double timeout_s, void *stream);
+void hiccl_program_destroy(hiccl_program_t *prog);
+
+/* ----------------------------------------------------------------------
  * Measurement utilities (bench.py; not part of the reference surface).
  *
  * fill_uniform: element i of buffer k = uniform [-1,1) value of hash

@@ -113,3 +113,17 @@ def test_header_is_c_and_plain_c_client_runs():
                         "-Wl,-rpath,/opt/rocm/lib"], check=True)
         p = subprocess.run([exe], capture_output=True, text=True)
         assert p.returncode == 0 and "abi_c: PASSED" in p.stdout, p.stdout + p.stderr
+
+
+def test_program_argument_checks_on_host():
+    """hiccl_program_*: NULL handles and unknown dtypes are refused before any
+    device work (no GPU here)."""
+    lib = L.lib()
+    h = ctypes.c_void_p()
+    assert lib.hiccl_program_create(None, L.HICCL_FLOAT32, 0) != 0
+    assert lib.hiccl_program_create(ctypes.byref(h), 99, 0) != 0 and not h.value
+    assert lib.hiccl_program_add_signal(None, None, 0, None, 0) != 0
+    assert lib.hiccl_program_add_plan(None, None, 0) != 0
+    assert lib.hiccl_program_launch(None, None, None, None, 1.0, None) != 0
+    assert lib.hiccl_program_num_segments(None) == 0 and lib.hiccl_program_num_phases(None) == 0
+    lib.hiccl_program_destroy(None)

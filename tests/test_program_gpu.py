@@ -1,0 +1,240 @@
+"""GPU tier: step programs (include/hiccl_reduce.h hiccl_program_*).
+
+A program runs an ordered list -- signal/wait phases, exact byte copies
+(HICCL_BYTES plans), reductions (plans of the program's dtype) -- as ONE
+launch, each element after the previous one completed.  HiCCL::Comm records
+one per stream-ordered pipeline step (comm.h:195-204's transport -> compute
+order).  The checks: a reduction sees the bytes the copy before it wrote
+(small shapes with half tiles, large with full tiles), a chain of dependent
+elements, phases store / await their per-launch epochs (and epoch +
+*epoch_dev under graph replay), a wait that is never satisfied times out
+with the error word set while the grid still drains, relaunches reuse the
+device counters, and the reductions give the oracle's bits.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import hiccl_amd
+from hiccl_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _copy_plan(dst, src, nbytes, dst_off=0, src_off=0):
+    c = hiccl_amd.Compute(torch.uint8, device=0)
+    c.add([(src.view(torch.uint8), src_off)], (dst.view(torch.uint8), dst_off), nbytes, compid=0)
+    return c
+
+
+def _sum_plan(out, ins, count, dtype=torch.float32):
+    c = hiccl_amd.Compute(dtype, device=0)
+    c.add(list(ins), out, count, compid=0)
+    return c
+
+
+def _inorder(xs):
+    acc = torch.zeros_like(xs[0])
+    for x in xs:  # T acc = 0; acc += in[k][i] (compute.h:7-9), one rounding per add
+        acc = acc + x
+    return acc
+
+
+@pytest.mark.parametrize("count", [(1 << 18) + 3, (1 << 24) + 5], ids=["half_tiles", "full_tiles"])
+def test_copy_then_reduce_sees_the_copy(count):
+    """[copy src -> mid] then [out = mid + b]: the reduction reads what the
+    copy wrote in the same launch (bits of an in-order sum), over three
+    launches with new source contents each time."""
+    src = torch.empty(count, device=DEV)
+    b = torch.empty(count, device=DEV)
+    mid = torch.full((count,), float("nan"), device=DEV)
+    out = torch.empty(count, device=DEV)
+    hiccl_amd.fill_uniform(b, 7, 1)
+    cp = _copy_plan(mid, src, count * 4)
+    red = _sum_plan(out, [mid, b], count)
+    prog = hiccl_amd.Program(torch.float32, device=0)
+    prog.add_plan(cp)
+    prog.add_plan(red)
+    assert prog.segments() == 2
+    for it in range(3):
+        hiccl_amd.fill_uniform(src, 100 + it, 0)
+        prog.launch()
+        torch.cuda.synchronize()
+        exp = _inorder([src, b])
+        assert torch.equal(mid.view(torch.int32), src.view(torch.int32))
+        assert torch.equal(out.view(torch.int32), exp.view(torch.int32)), f"launch {it}"
+    prog.close()
+
+
+def test_dependent_chain_of_elements():
+    """out_k = out_{k-1} + x_k for 12 elements, alternating with byte copies
+    and self-signalling phases: every element must see its predecessor."""
+    count = (1 << 20) + 7
+    xs = [torch.empty(count, device=DEV) for _ in range(12)]
+    for k, x in enumerate(xs):
+        hiccl_amd.fill_uniform(x, 11, k)
+    outs = [torch.empty(count, device=DEV) for _ in range(12)]
+    flags = torch.zeros(64, dtype=torch.int32, device=DEV)
+    prog = hiccl_amd.Program(torch.float32, device=0)
+    keep = []
+    prev = None
+    nph = 0
+    for k in range(12):
+        if prev is None:
+            c = _sum_plan(outs[k], [xs[k]], count)
+        else:
+            c = _sum_plan(outs[k], [prev, xs[k]], count)
+        keep.append(c)
+        prog.add_plan(c)
+        if k % 3 == 1:  # a copy of the running sum, then a phase
+            cp_dst = torch.empty(count, device=DEV)
+            cp = _copy_plan(cp_dst, outs[k], count * 4)
+            keep += [cp, cp_dst]
+            prog.add_plan(cp)
+            f = flags.data_ptr() + 4 * nph
+            prog.add_signal([f], [f])
+            nph += 1
+            prev = cp_dst
+        else:
+            prev = outs[k]
+    epochs = list(range(40, 40 + nph))
+    prog.launch(epochs)
+    torch.cuda.synchronize()
+    acc = torch.zeros(count, device=DEV)
+    for k in range(12):
+        acc = acc + xs[k]
+        assert torch.equal(outs[k].view(torch.int32), acc.view(torch.int32)), f"element {k}"
+    assert flags[:nph].tolist() == epochs
+    prog.close()
+
+
+def test_phases_store_and_await_epochs_and_relaunch():
+    count = 1 << 16
+    x = torch.empty(count, device=DEV)
+    hiccl_amd.fill_uniform(x, 3, 0)
+    out = torch.empty(count, device=DEV)
+    flags = torch.zeros(8, dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    fa, fb = flags.data_ptr(), flags.data_ptr() + 4
+    prog = hiccl_amd.Program(torch.float32, device=0)
+    prog.add_signal([fa], [fa])
+    red = _sum_plan(out, [x, x], count)
+    prog.add_plan(red)
+    prog.add_signal([fb], [fb])
+    assert prog.phases() == 2 and prog.segments() == 3
+    for e in (5, 9, 13):
+        prog.launch([e, e + 1], err=err.data_ptr(), timeout_s=5.0)
+        torch.cuda.synchronize()
+        assert flags[:2].tolist() == [e, e + 1]
+        assert err.item() == 0
+    assert torch.equal(out.view(torch.int32), (torch.zeros_like(x) + x + x).view(torch.int32))
+    prog.close()
+
+
+def test_unsatisfied_wait_times_out_and_drains():
+    """A phase waiting for a flag nobody sets: after timeout_s the error word
+    is set and the launch finishes (every later element still runs)."""
+    count = 1 << 16
+    x = torch.empty(count, device=DEV)
+    hiccl_amd.fill_uniform(x, 5, 0)
+    out = torch.zeros(count, device=DEV)
+    flags = torch.zeros(4, dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    prog = hiccl_amd.Program(torch.float32, device=0)
+    prog.add_signal([], [flags.data_ptr()])
+    red = _sum_plan(out, [x], count)
+    prog.add_plan(red)
+    prog.launch([1], err=err.data_ptr(), timeout_s=0.2)
+    torch.cuda.synchronize()
+    assert err.item() != 0
+    assert torch.equal(out.view(torch.int32), (torch.zeros_like(x) + x).view(torch.int32))
+    prog.close()
+
+
+def test_graph_replay_reads_epoch_counter():
+    """Eager launch first (uploads the tables), then the launch captured into
+    a graph with epoch_dev: replay r stores / awaits epoch + r."""
+    count = 1 << 16
+    x = torch.empty(count, device=DEV)
+    hiccl_amd.fill_uniform(x, 9, 0)
+    out = torch.empty(count, device=DEV)
+    flags = torch.zeros(4, dtype=torch.int32, device=DEV)
+    ctr = torch.zeros(1, dtype=torch.int32, device=DEV)
+    f = flags.data_ptr()
+    prog = hiccl_amd.Program(torch.float32, device=0)
+    prog.add_signal([f], [f])
+    red = _sum_plan(out, [x, x, x], count)
+    prog.add_plan(red)
+    prog.launch([100])
+    torch.cuda.synchronize()
+    assert flags[0].item() == 100
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            cs = torch.cuda.current_stream()
+            L.check(L.lib().hiccl_counter_add(ctypes.c_void_p(ctr.data_ptr()), 1, ctypes.c_void_p(cs.cuda_stream)),
+                    "counter_add")
+            prog.launch([100], epoch_dev=ctr.data_ptr(), stream=cs)
+    for r in range(1, 4):
+        g.replay()
+        torch.cuda.synchronize()
+        assert ctr.item() == r and flags[0].item() == 100 + r
+    exp = torch.zeros_like(x) + x + x + x
+    assert torch.equal(out.view(torch.int32), exp.view(torch.int32))
+    del g
+    prog.close()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float64, torch.int64], ids=["bf16", "f64", "u64"])
+def test_program_dtypes_match_oracle(oracle, dtype):
+    count = (1 << 17) + 9
+    n = 5
+    fill_as = torch.float64 if dtype == torch.int64 else dtype
+    ins = [torch.empty(count, dtype=fill_as, device=DEV) for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, 21, k)
+    ins = [t.view(dtype) for t in ins]
+    out = torch.empty(count, dtype=dtype, device=DEV)
+    prog = hiccl_amd.Program(dtype, device=0)
+    red = _sum_plan(out, ins, count, dtype)
+    prog.add_plan(red)
+    prog.launch()
+    ref = torch.empty_like(out)
+    hiccl_amd.reduce(ref, ins)
+    torch.cuda.synchronize()
+    iv = {torch.bfloat16: torch.int16, torch.float64: torch.int64, torch.int64: torch.int64}[dtype]
+    assert torch.equal(out.view(iv), ref.view(iv))
+    if dtype == torch.float64:
+        host = np.stack([t.cpu().numpy() for t in ins])
+        exp = oracle.reduce(host)
+        assert np.array_equal(out.cpu().numpy().view(np.uint64), exp.view(np.uint64))
+    prog.close()
+
+
+def test_joined_plans_and_refusals():
+    count = 1 << 18
+    a = torch.empty(count, device=DEV)
+    b = torch.empty(count, device=DEV)
+    hiccl_amd.fill_uniform(a, 1, 0)
+    hiccl_amd.fill_uniform(b, 1, 1)
+    o1 = torch.empty(count, device=DEV)
+    o2 = torch.empty(count, device=DEV)
+    prog = hiccl_amd.Program(torch.float32, device=0)
+    p1, p2 = _sum_plan(o1, [a, b], count), _sum_plan(o2, [b, a], count)
+    prog.add_plan(p1)
+    prog.add_plan(p2, join=True)
+    assert prog.segments() == 1
+    prog.launch()
+    torch.cuda.synchronize()
+    assert torch.equal(o1.view(torch.int32), _inorder([a, b]).view(torch.int32))
+    assert torch.equal(o2.view(torch.int32), _inorder([b, a]).view(torch.int32))
+    # a plan of another reduction dtype is refused (bytes plans are accepted)
+    bad = _sum_plan(torch.empty(count, dtype=torch.float64, device=DEV),
+                    [torch.zeros(count, dtype=torch.float64, device=DEV)], count, torch.float64)
+    with pytest.raises(hiccl_amd.HicclError):
+        prog.add_plan(bad)
+    prog.close()
