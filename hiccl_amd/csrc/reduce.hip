@@ -2107,6 +2107,7 @@ struct hiccl_program {
   ProgArgs args;
   int unroll = 4;
   uint32_t grid = 0;
+  uint32_t max_wg = 0;  // hiccl_program_set_max_workgroups (0: CUs x kProgBpc)
   std::atomic<bool> enqueued{false};
 };
 
@@ -2172,7 +2173,8 @@ int prog_upload(hiccl_program *p, hipStream_t s) {
   p->unroll = pick_prog(p->dtype, 2) && total_pkt < 2ull * cus * kProgBlock * 4 ? 2 : 4;
   const uint64_t unit = (uint64_t)kProgBlock * p->unroll;
   // the units of every segment, in order, and the ticket layout
-  const uint32_t grid_cap = (uint32_t)(cus * kProgBpc);
+  uint32_t grid_cap = (uint32_t)(cus * kProgBpc);
+  if (p->max_wg && p->max_wg < grid_cap) grid_cap = p->max_wg;
   std::vector<uint32_t> unit_comp;
   std::vector<PlanDesc> desc(ncomp);
   std::vector<const void *> ptrs(ncomp * maxn, nullptr);
@@ -2328,6 +2330,14 @@ int hiccl_program_add_plan(hiccl_program_t *p, const hiccl_reduce_plan_t *plan, 
     p->segs.push_back(hiccl_program::Seg{0, {}, 0, 0});
   }
   for (auto &c : plan->comps) p->segs.back().units.push_back(hiccl_program::Unit{c.out, c.in, c.count, bytes});
+  p->dirty = true;
+  return 0;
+}
+
+int hiccl_program_set_max_workgroups(hiccl_program_t *p, int max_wg) {
+  if (!p) return fail(hipErrorInvalidValue, "program_set_max_workgroups: prog is NULL");
+  if (max_wg < 0) return fail(hipErrorInvalidValue, "program_set_max_workgroups: max_wg < 0");
+  p->max_wg = (uint32_t)max_wg;
   p->dirty = true;
   return 0;
 }

@@ -230,6 +230,7 @@ class Comm {
     libs = libraries_used(coll_batch);
     steps = merge_steps(coll_batch, libs, 1);
 #ifndef HICCL_PORT_HOST
+    device_ranks = CommBench::ranks_on_my_device();
     shared_device = CommBench::ranks_share_device();
     if (std::find(libs.begin(), libs.end(), CommBench::XCCL) != libs.end()) {
       xccl = CommBench::xccl_setup(shared_device);
@@ -422,6 +423,7 @@ class Comm {
   int stream_req = -1;  // -1: decide from the environment and the node layout; 2: forced
   bool streamed = false;
   bool shared_device = false;  // two or more ranks drive one GPU
+  int device_ranks = 1;        // ranks driving this rank's GPU (this one included)
   bool xccl = false;           // XCCL levels run on RCCL
   int fuse_req = -1;  // -1: HICCL_FUSED_GATHER
   bool fused = false;
@@ -496,6 +498,11 @@ class Comm {
       CommBench::StepRecorder rec;
       if (hiccl_program_create(&rec.prog, dtype_of<T>(), CommBench::mydevice))
         CommBench::die("step program", hiccl_last_error());
+      // A program's workgroups wait for their predecessors on the GPU; ranks
+      // sharing it (single-GPU rehearsals only) split its workgroup slots so
+      // every rank's program stays resident while the others wait for it.
+      if (device_ranks > 1 && hiccl_program_set_max_workgroups(rec.prog, program_grid_share()))
+        CommBench::die("step program", hiccl_last_error());
       CommBench::step_recorder() = &rec;
       for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
       for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
@@ -512,6 +519,15 @@ class Comm {
     if (hiccl_program_launch(sp.prog, epochs.data(), in_capture ? graph_ctr : nullptr, flags.err, CommBench::signal_timeout(),
                              s))
       CommBench::die("step program", hiccl_last_error());
+  }
+
+  int program_grid_share() const {
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, CommBench::mydevice) != hipSuccess) {
+      (void)hipGetLastError();
+      cus = 256;
+    }
+    return std::max(8, cus / device_ranks);
   }
 
   bool want_programs() {

@@ -138,7 +138,8 @@ inline void init() {
 // device (same host, same PCI bus id): CommBench::init assigns devices
 // round-robin, so a node with more ranks than GPUs shares them.
 // Collective over comm_mpi.
-inline bool ranks_share_device() {
+// Every rank's "host/PCI bus id" (collective over comm_mpi).
+inline std::vector<std::string> device_keys() {
   char key[192];
   std::memset(key, 0, sizeof(key));
   char host[96] = {0};
@@ -151,8 +152,17 @@ inline bool ranks_share_device() {
             "MPI_Allgather(device keys)");
   std::vector<std::string> keys;
   for (int r = 0; r < numproc; r++) keys.emplace_back(all.data() + (size_t)r * sizeof(key));
+  return keys;
+}
+inline bool ranks_share_device() {
+  std::vector<std::string> keys = device_keys();
   std::sort(keys.begin(), keys.end());
   return std::adjacent_find(keys.begin(), keys.end()) != keys.end();
+}
+// Ranks (this one included) driving this rank's device.  Collective.
+inline int ranks_on_my_device() {
+  const std::vector<std::string> keys = device_keys();
+  return (int)std::count(keys.begin(), keys.end(), keys[myid]);
 }
 
 // ------------------------------------------------------------- RCCL ------

@@ -315,6 +315,10 @@ int hiccl_program_create(hiccl_program_t **prog, int dtype, int device);
 int hiccl_program_add_signal(hiccl_program_t *prog, uint32_t *const *sig, int nsig, const uint32_t *const *wait,
                              int nwait);
 int hiccl_program_add_plan(hiccl_program_t *prog, const hiccl_reduce_plan_t *plan, int join);
+/* Cap the launch at max_wg workgroups (0: the default, 2 per CU).  Several
+ * processes sharing one GPU (rehearsals) split it this way: a program's
+ * workgroups wait on the GPU for earlier elements and peers' tokens. */
+int hiccl_program_set_max_workgroups(hiccl_program_t *prog, int max_wg);
 int hiccl_program_num_segments(const hiccl_program_t *prog);
 int hiccl_program_num_phases(const hiccl_program_t *prog);
 int hiccl_program_launch(hiccl_program_t *prog, const uint32_t *epochs, const uint32_t *epoch_dev, uint32_t *err,
