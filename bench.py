@@ -165,7 +165,11 @@ def run_c5(world, args, allow_shared=False):
     fused = {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "1"}
     modes = [("host", {"HICCL_STREAM_ORDERED": "0"}, hier, libs),
              ("stream_graph", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "0"}, hier, libs),
-             ("stream_graph_fused", fused, hier, libs)]
+             ("stream_graph_fused", fused, hier, libs),
+             # the same with one launch per element of a step instead of one
+             # step program per step: the A/B of the
+             # round-3 change across GPUs
+             ("stream_graph_fused_noprog", dict(fused, HICCL_STEP_PROGRAM="0"), hier, libs)]
     # the reference's main.cu runs its levels on XCCL (main.cu:25): RCCL
     # point-to-point per level, opted into here (HICCL_XCCL=rccl; on shared
     # GPUs the library falls back to IPC, and mode_used says which ran)
@@ -204,10 +208,15 @@ def run_c5(world, args, allow_shared=False):
         finally:
             os.unlink(path)
         r["wall_s"] = round(time.perf_counter() - t0, 1)
+        r["rc"] = p.returncode
         out[name] = r
         log(f"bench: c5 {name}: {r}")
-        if p.returncode != 0:
-            break  # a failure, crash or time-out: start nothing more on the GPUs
+        if p.returncode < 0 or p.returncode in (124, 137) or p.returncode >= 128:
+            # killed at its limit, hung or crashed: start nothing more on the
+            # GPUs (a mode that failed its check or its own signal time-out
+            # exits 1 and leaves the GPUs usable: the next mode still runs)
+            out["stopped_after"] = name
+            break
     return out
 
 
@@ -857,6 +866,14 @@ def schedsweep(args):
                     ("tile_u8_dyn", dict(engine=1, unroll=8, schedule=2, grab=1)),
                     ("tile_u8_dyn_g2", dict(engine=1, unroll=8, schedule=2, grab=2)),
                     ("tile_u16_dyn", dict(engine=1, unroll=16, schedule=2, grab=1))]
+    if args.sweepset == "c3":  # config 3 per n: engine / occupancy / tile size
+        variants = [("auto", None),
+                    ("tile_dyn", dict(engine=1, schedule=2)),
+                    ("tile_dyn_bpc2", dict(engine=1, schedule=2, blocks_per_cu=2)),
+                    ("tile_dyn_u2_bpc2", dict(engine=1, schedule=2, unroll=2, blocks_per_cu=2)),
+                    ("tile_static", dict(engine=1, schedule=1)),
+                    ("phase_static", dict(engine=2, schedule=1)),
+                    ("phase_dyn", dict(engine=2, schedule=2))]
     if args.sweepset == "xover":  # engine x schedule crossover (sets AUTO)
         variants = [("auto", None),
                     ("tile_dyn", dict(engine=1, schedule=2)),

@@ -22,11 +22,17 @@ def test_c5_leg_rehearsal_one_gpu(ranks):
     import bench
     res = bench.run_c5(ranks, argparse.Namespace(c5_log2count=14, c5_iters=2), allow_shared=True)
     assert "workload" in res, res
-    modes = ["host", "stream_graph", "stream_graph_fused", "xccl"] + (["flat_stream_graph_fused"] if ranks > 2 else [])
-    assert [m for m in res if m.endswith(("host", "fused", "graph", "xccl"))] == modes
+    modes = (["host", "stream_graph", "stream_graph_fused", "stream_graph_fused_noprog", "xccl"]
+             + (["flat_stream_graph_fused"] if ranks > 2 else []))
+    assert [m for m in res if m.endswith(("host", "fused", "graph", "xccl", "noprog"))] == modes
+    assert res["devices_counted_unmasked"] >= 1 and isinstance(res["env_scrubbed"], dict)
     for mode in modes:
         r = res[mode]
         assert r.get("kat") == "PASSED", r
+        assert r["rc"] == 0 and len(r["devices_seen"]) == ranks and len(r["bus_ids"]) == ranks
+        assert len(set(r["bus_ids"])) == 1 and "ranks share a GPU" in r["mode_used"]  # one GPU here
+        if mode == "xccl":
+            assert "xccl-rccl" not in r["mode_used"]  # RCCL refuses a shared GPU: the IPC path ran
         assert r["ranks"] == ranks and r["pipedepth"] == 128
         assert r["hierarchy"] == (str(ranks) if mode.startswith("flat") or ranks == 2 else f"1,{ranks // 2},2")
         assert r["collective_ms_median"] > 0 and r["algorithmic_GBps_median"] > 0
