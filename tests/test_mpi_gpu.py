@@ -115,6 +115,36 @@ def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ri
         assert got.tobytes() == exp.tobytes(), f"rank {r}: {int((got != exp).sum())} differ"
 
 
+@pytest.mark.parametrize("np_,count,depth,hier,libs", [(2, 65536, 4, "2", "ipc"), (8, 4099, 4, "1,4,2", "mpi,ipc,ipc")])
+@pytest.mark.parametrize("fused,graph", [(False, False), (True, True)], ids=["stream", "stream-fused-graph"])
+@pytest.mark.parametrize("program", ["0", "1"], ids=["per_element", "step_program"])
+def test_allreduce_bits_step_program_ab(tmp_path, oracle, np_, count, depth, hier, libs, fused, graph, program):
+    """Stream-ordered mode with one step program per pipeline step (the
+    default) and with one launch per element
+    (HICCL_STEP_PROGRAM=0): the same bits as oracle/schedule.py either way."""
+    prefix = str(tmp_path / "ar")
+    rc, out = mpirun(np_, HIP_F32, [8, count, 1, 1, depth, 0, 0, hier, libs, prefix], streamed=True, fused=fused,
+                     graph=graph, repeat=4 if graph else 2, extra_env={"HICCL_STEP_PROGRAM": program})
+    assert rc == 0, out[-3000:]
+    assert ("step programs: one launch per step" in out) == (program == "1"), out[-2000:]
+    n = count * np_
+    x = {r: oracle.fill(r + 1, n, 1234)[r] for r in range(np_)}
+    libmap = {"mpi": S.MPI, "ipc": S.IPC, "ipc_get": S.IPC_GET}
+    sch = S.Schedule(np_, [int(h) for h in hier.split(",")], [libmap[lv] for lv in libs.split(",")],
+                     numstripe=1, ringnodes=1, pipedepth=depth, ring_reuse_fix=True)
+    S.compose("allreduce", np_, count)(sch)
+    steps = sch.init()
+    user = {}
+    for r in range(np_):
+        user[(r, ("send",))] = x[r]
+        user[(r, ("recv",))] = np.full(n, -1.0, np.float32)
+    mem = S.simulate(steps, np_, user)
+    for r in range(np_):
+        got = np.fromfile(f"{prefix}.rank{r}.bin", dtype=np.float32)
+        exp = mem[(r, ("recv",))]
+        assert got.tobytes() == exp.tobytes(), f"rank {r}: {int((got != exp).sum())} differ"
+
+
 @pytest.mark.parametrize("np_,hier,libs", [(2, "2", "ipc"), (4, "2,2", "mpi,ipc"), (4, "4", "ipc_get"),
                                            (8, "1,4,2", "mpi,ipc,ipc")])
 @pytest.mark.parametrize("pattern", [4, 8])
