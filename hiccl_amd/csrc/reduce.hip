@@ -788,6 +788,8 @@ struct ProgArgs {
   const uint32_t *epoch_dev;
   uint64_t timeout_ticks;
   uint32_t stride, nseg, nticket, nphase;
+  uint32_t fences;  // measurement only (HICCL_PROGRAM_FENCES): bit 0 skips the release, bit 1 the acquire fences
+  uint32_t pad;
   ProgSeg seg[kProgMaxSegs];
   uint32_t epoch[kProgMaxPhases];  // per launch: phase p stores / awaits epoch[p] (+ *epoch_dev)
 };
@@ -795,9 +797,12 @@ struct ProgArgs {
 // Bounded spin of one lane until *c >= need: false on time-out or an error
 // recorded by anyone (then *err is set and the caller goes on without
 // waiting, so the grid always drains).
+// The poll is a RELAXED load: an acquire load invalidates the XCD's L2 on
+// every poll (buffer_inv sc1), and hundreds of waiting workgroups doing that
+// starve the ones at work; the caller takes one acquire fence after the wait.
 __device__ __forceinline__ void prog_gate_wait(const ProgArgs &a, const uint32_t *c, uint32_t need) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need) {
+  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
     __builtin_amdgcn_s_sleep(1);
     if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
     if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
@@ -820,7 +825,8 @@ __device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t first, u
     for (uint32_t i = w0 + lane; i < w1; i += 64) {
       const uint32_t *f = ((const uint32_t *const __attribute__((address_space(4))) *)a.wait)[i];
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while ((int32_t)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      // relaxed polls (no cache invalidate per poll); the fence below acquires
+      while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
         __builtin_amdgcn_s_sleep(2);
         if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
@@ -864,9 +870,9 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
   uint32_t open = 0;               // segments below `open` are complete, as this workgroup has seen
   uint32_t pend_seg = 0, pend = 0;  // completions of pend_seg done here, not yet published
   auto publish = [&]() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this wave's stores done and written back (system scope)
+    if (!(a.fences & 1u)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this wave's stores done, written back
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&a.ctr[2 + pend_seg], pend, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_add(&a.ctr[2 + pend_seg], pend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     pend = 0;
   };
   while (k < a.nticket) {
@@ -879,7 +885,7 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
     if (s > open) {
       if (tid == 0) prog_gate_wait(a, &a.ctr[2 + s - 1], a.seg[s - 1].need);
       __syncthreads();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // see what the completed segments (and peers) wrote
+      if (!(a.fences & 2u)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // see what they (and peers) wrote
       open = s;
     }
     const uint32_t kind = a.seg[s].kind, first = a.seg[s].first, count = a.seg[s].count;
@@ -2361,6 +2367,11 @@ int hiccl_program_launch(hiccl_program_t *p, const uint32_t *epochs, const uint3
   a.epoch_dev = epoch_dev;
   a.timeout_ticks = (uint64_t)((timeout_s > 0 ? timeout_s : 30.0) * 1e8);  // s_memrealtime: 100 MHz
   for (uint32_t i = 0; i < a.nphase; i++) a.epoch[i] = epochs[i];
+  static const uint32_t fences = [] {
+    const char *e = getenv("HICCL_PROGRAM_FENCES");  // measurement only: see ProgArgs::fences
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  a.fences = fences;
   fn(a, dim3(p->grid), s);
   p->enqueued.store(true, std::memory_order_relaxed);
   return check_hip(hipGetLastError(), "program_launch: launch");

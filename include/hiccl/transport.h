@@ -386,10 +386,9 @@ struct IpcExport {
 // retired mapping is revived when the peer exports the same allocation
 // again (same base, not recycled) and closed, oldest first, only when the
 // retired mappings exceed the cap or on ipc_trim().  The cap
-// (HICCL_IPC_RETIRED_MAX bytes) defaults to twice the largest set of peer
-// allocations this process has had mapped at once: at most two generations
-// of a communicator's peer buffers stay alive after they are freed, never
-// more than a fixed share of HBM.  A mapping opened for a recycled address is
+// (HICCL_IPC_RETIRED_MAX bytes) is tied to what this process maps
+// (ipc_retired_max): a bounded number of generations of its peers' buffers
+// stay alive after they are freed, never more than a quarter of HBM.  A mapping opened for a recycled address is
 // verified by a probe (ipc_probe_*), so a closed-then-reopened address that
 // misses fails loudly instead of losing data.
 struct IpcMapping {
@@ -426,13 +425,32 @@ inline size_t &ipc_live_peak() {
   static size_t b = 0;
   return b;
 }
+// Default cap: kIpcRetiredGenerations x the most peer memory this process
+// has had mapped at once, at least 256 MiB, at most a quarter of the
+// device's memory.  Measured (round 3): at 2 x, the 4-rank test that
+// recreates communicators on freshly allocated buffers every round
+// (test_recreated_communicators_on_reallocated_buffers) was stopped by the
+// recycled-address probe in round 3 of 5 -- closes the cap forces meet the
+// runtime behaviour the retirement avoids -- so the cap keeps many
+// generations; a job that outgrows it is stopped by the probe, never
+// silently wrong.
+constexpr size_t kIpcRetiredGenerations = 16;
 inline size_t ipc_retired_max() {
   static const long long env = [] {
     const char *e = std::getenv("HICCL_IPC_RETIRED_MAX");
     return e ? (long long)std::strtoull(e, nullptr, 0) : -1ll;
   }();
   if (env >= 0) return (size_t)env;
-  return 2 * ipc_live_peak();
+  static const size_t ceiling = [] {
+    size_t fr = 0, total = 0;
+    if (hipMemGetInfo(&fr, &total) != hipSuccess) {
+      (void)hipGetLastError();
+      return (size_t)16 << 30;
+    }
+    return total / 4;
+  }();
+  const size_t want = std::max(kIpcRetiredGenerations * ipc_live_peak(), (size_t)256 << 20);
+  return std::min(want, ceiling);
 }
 
 // HICCL_DEBUG_IPC=1: every export, import and close on stdout; =2: kept in
