@@ -1037,6 +1037,22 @@ def progstep(args):
 
     runs = {"separate": separate, "program": program, "separate_no_phases": separate_nophase,
             "program_no_phases": program_nophase}
+    # the program at fewer workgroups (fewer ticket / completion atomics)
+    progs_wg = []
+    for wg in (256, 128, 64):
+        pw = hiccl_amd.Program(torch.float32, device=dev)
+        pw.add_signal([f[0]], [f[0]])
+        pw.add_plan(cp)
+        pw.add_signal([f[1]], [f[1]])
+        pw.add_plan(comp)
+        pw.add_signal([f[2]], [f[2]])
+        pw.set_max_workgroups(wg)
+        progs_wg.append(pw)
+
+        def run_wg(pw=pw):
+            epoch[0] += 1
+            pw.launch([epoch[0]] * 3, err=err.data_ptr(), timeout_s=10.0, stream=stream)
+        runs[f"program_wg{wg}"] = run_wg
     res = {k: [] for k in runs}
     for _ in range(5):
         for k, fn in runs.items():
@@ -1059,6 +1075,8 @@ def progstep(args):
     print(json.dumps(row), flush=True)
     prog.close()
     prog2.close()
+    for pw in progs_wg:
+        pw.close()
     return 0
 
 

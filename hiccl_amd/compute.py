@@ -270,6 +270,10 @@ class Program:
         L.check(L.lib().hiccl_program_add_plan(self._prog, compute._plan, 1 if join else 0), "program_add_plan")
         self._keep.append(compute)
 
+    def set_max_workgroups(self, n):
+        """Cap the launch at ``n`` workgroups (0: 2 per CU)."""
+        L.check(L.lib().hiccl_program_set_max_workgroups(self._prog, int(n)), "program_set_max_workgroups")
+
     def segments(self):
         return L.lib().hiccl_program_num_segments(self._prog)
 

@@ -762,6 +762,10 @@ constexpr int kProgMaxSegs = 48;
 constexpr int kProgMaxPhases = 64;
 constexpr int kProgBlock = 256;
 constexpr int kProgPol = 11;  // nt loads, nt stores (the library's default policy)
+// Counters 256 B apart: the ticket counter's atomics must not share a line
+// with the completion counters that waiting workgroups poll.
+constexpr int kCtrStride = 64;  // uint32 words
+constexpr size_t kCtrBytes = (size_t)(2 + kProgMaxSegs) * kCtrStride * 4;
 
 struct ProgSeg {
   uint32_t tick_begin;  // first ticket (segment s owns [tick_begin, seg[s+1].tick_begin))
@@ -783,7 +787,7 @@ struct ProgArgs {
   const ProgPhase *phase;
   uint32_t *const *sig;
   const uint32_t *const *wait;
-  uint32_t *ctr;  // [0] tickets, [1] exits, [2 + s] completions of segment s; zero between launches
+  uint32_t *ctr;  // [0] tickets, [1] exits, [2 + s] completions of segment s (x kCtrStride); zero between launches
   uint32_t *err;
   const uint32_t *epoch_dev;
   uint64_t timeout_ticks;
@@ -802,8 +806,10 @@ struct ProgArgs {
 // starve the ones at work; the caller takes one acquire fence after the wait.
 __device__ __forceinline__ void prog_gate_wait(const ProgArgs &a, const uint32_t *c, uint32_t need) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t nap = 1;  // backoff: fewer polls of one line from hundreds of waiting workgroups
   while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-    __builtin_amdgcn_s_sleep(1);
+    for (uint32_t i = 0; i < nap; i++) __builtin_amdgcn_s_sleep(2);
+    if (nap < 16) nap <<= 1;
     if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
     if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
       if (a.err) __hip_atomic_store(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -863,7 +869,7 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
   for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * kProgBlock + tid) * kPacket);
   __shared__ uint32_t s_tick[2];
   const uint32_t add = a.epoch_dev ? __hip_atomic_load(a.epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-  if (tid == 0) s_tick[0] = __hip_atomic_fetch_add(&a.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) s_tick[0] = __hip_atomic_fetch_add(&a.ctr[0 * kCtrStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   uint32_t k = __builtin_amdgcn_readfirstlane(s_tick[0]);  // workgroup-uniform: scalar from here on
   int slot = 0;
@@ -872,7 +878,7 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
   auto publish = [&]() {
     if (!(a.fences & 1u)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this wave's stores done, written back
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&a.ctr[2 + pend_seg], pend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_add(&a.ctr[(2 + pend_seg) * kCtrStride], pend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     pend = 0;
   };
   while (k < a.nticket) {
@@ -880,10 +886,10 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
     while (s + 1 < a.nseg && a.seg[s + 1].tick_begin <= k) s++;
     // the next ticket, taken before this one's work (its latency hides under it)
     uint32_t nxt = 0;
-    if (tid == 0) nxt = __hip_atomic_fetch_add(&a.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) nxt = __hip_atomic_fetch_add(&a.ctr[0 * kCtrStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (pend && pend_seg != s) publish();  // before any wait: others may be waiting for it
     if (s > open) {
-      if (tid == 0) prog_gate_wait(a, &a.ctr[2 + s - 1], a.seg[s - 1].need);
+      if (tid == 0) prog_gate_wait(a, &a.ctr[(2 + s - 1) * kCtrStride], a.seg[s - 1].need);
       __syncthreads();
       if (!(a.fences & 2u)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // see what they (and peers) wrote
       open = s;
@@ -920,12 +926,12 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
   if (tid == 0) {
     // every ticket take of this workgroup precedes its exit increment; the
     // last one out leaves the counters zero for the next launch
-    const uint32_t prev = __hip_atomic_fetch_add(&a.ctr[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t prev = __hip_atomic_fetch_add(&a.ctr[1 * kCtrStride], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == gridDim.x - 1) {
-      __hip_atomic_store(&a.ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&a.ctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.ctr[0 * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.ctr[1 * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (uint32_t s = 0; s < a.nseg; s++)
-        __hip_atomic_store(&a.ctr[2 + s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.ctr[(2 + s) * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -2160,8 +2166,8 @@ int prog_upload(hiccl_program *p, hipStream_t s) {
     p->d_block = nullptr;
   }
   if (!p->d_ctr) {
-    if (int e = check_hip(hipMalloc((void **)&p->d_ctr, 256), "program: hipMalloc(counters)")) return e;
-    if (int e = check_hip(hipMemset(p->d_ctr, 0, 256), "program: hipMemset(counters)")) return e;
+    if (int e = check_hip(hipMalloc((void **)&p->d_ctr, kCtrBytes), "program: hipMalloc(counters)")) return e;
+    if (int e = check_hip(hipMemset(p->d_ctr, 0, kCtrBytes), "program: hipMemset(counters)")) return e;
   }
   const int cus = device_cus(p->device);
   const size_t tesz = esize(p->dtype);

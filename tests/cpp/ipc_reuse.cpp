@@ -1,22 +1,25 @@
-// tests/cpp/ipc_reuse.cpp -- standalone two-process reproducer of the HIP IPC
-// behaviour the transport works around (include/hiccl/transport.h,
-// IpcMapping: released mappings are retired, not closed).
+// tests/cpp/ipc_reuse.cpp -- standalone reproducer of the HIP IPC behaviour
+// the transport works around (include/hiccl/transport.h, IpcMapping:
+// released mappings are retired, not closed).
 //
-// Rank 0 (owner) and rank 1 (importer), one device each (or both on device 0
-// of a one-GPU box).  Per round, with `nbuf` buffers of `bytes` each:
-//   1. owner: hipMalloc A[0..nbuf), write nonce a_j into each, export each
-//   2. importer: open each, read a_j (copy engine and a kernel), then, in
-//      variant "close", hipIpcCloseMemHandle each -- in "keep", leave them open
-//   3. owner: hipFree A[*], hipMalloc B[0..nbuf) of the same sizes (the
-//      allocator usually hands A's addresses back), write nonces b_j, export
-//   4. importer: open B[*], read b_j through the new mappings (copy engine
-//      and a kernel: hiccl_stream_copy), record whether each view saw b_j
-// Small buffers (1 MiB) are sub-allocated by HIP from larger chunks, large
-// ones (64 MiB) are allocations of their own; the transport sees both (user
-// buffers, schedule buffers).  The reference exchanges hipIpcMemHandle_t
+// P processes (2..8; one device each, or all on device 0 of a one-GPU box),
+// all-to-all like a communicator.  Per round, with `nbuf` buffers of
+// `bytes` on every rank:
+//   1. every rank hipMallocs A[0..nbuf), writes a nonce into each and
+//      exports them to every other rank
+//   2. every rank opens every peer's A, reads the nonces (copy engine and a
+//      kernel), then releases the mappings by the case's policy: "close"
+//      (hipIpcCloseMemHandle all), "keep" (leave all open), "mixed" (odd
+//      ranks keep, even ranks close)
+//   3. every rank hipFrees A and hipMallocs B of the same sizes (the
+//      allocator usually hands A's addresses back), writes nonces, exports
+//   4. every rank opens every peer's B and reads its nonces through the new
+//      mappings, then closes them
+// Small buffers (1 MiB) are sub-allocated by HIP, large ones (64 MiB) are
+// allocations of their own.  The reference exchanges hipIpcMemHandle_t
 // across processes the same way (/root/reference/misc/test.md:85).
 //
-//   mpirun -np 2 build/ipc_reuse <rounds>   -> one JSON line per case
+//   mpirun -np P build/ipc_reuse <rounds>   -> one JSON line per case (rank 0)
 #include <hip/hip_runtime_api.h>
 #include <mpi.h>
 
@@ -42,8 +45,8 @@ struct Export {
   uint64_t nonce;
 };
 
-// importer: read the first 8 bytes of `p` with the copy engine and with a
-// kernel; bit 0 = copy engine saw `want`, bit 1 = kernel saw `want`
+// read the first 8 bytes of `p` with the copy engine and with a kernel;
+// bit 0 = copy engine saw `want`, bit 1 = kernel saw `want`
 static int read_views(const void *p, uint64_t want, uint64_t *scratch) {
   uint64_t got = 0, got_k = 0;
   check(hipMemcpy(&got, p, 8, hipMemcpyDeviceToHost), "read (copy engine)");
@@ -56,24 +59,27 @@ static int read_views(const void *p, uint64_t want, uint64_t *scratch) {
   return (got == want ? 1 : 0) | (got_k == want ? 2 : 0);
 }
 
-static uint64_t next_nonce() {
+static uint64_t next_nonce(int me) {
   static uint64_t seq = 0x9e3779b97f4a7c15ull;
-  seq = seq * 6364136223846793005ull + 1442695040888963407ull;
+  seq = seq * 6364136223846793005ull + 1442695040888963407ull + (uint64_t)me;
   return seq;
 }
 
-// owner: nbuf fresh allocations with nonces, exported to rank 1
-static std::vector<void *> owner_round(size_t bytes, int nbuf, int tag) {
+// this rank's nbuf fresh allocations with nonces; every rank's exports
+static std::vector<void *> alloc_and_export(size_t bytes, int nbuf, int me, int np, std::vector<Export> &all) {
   std::vector<void *> a(nbuf);
-  std::vector<Export> e(nbuf);
+  std::vector<Export> mine(nbuf);
   for (int j = 0; j < nbuf; j++) {
     check(hipMalloc(&a[j], bytes), "hipMalloc");
-    e[j].nonce = next_nonce();
-    check(hipMemcpy(a[j], &e[j].nonce, 8, hipMemcpyHostToDevice), "write nonce");
-    check(hipIpcGetMemHandle(&e[j].h, a[j]), "export");
-    e[j].addr = (uint64_t)(uintptr_t)a[j];
+    mine[j].nonce = next_nonce(me);
+    check(hipMemcpy(a[j], &mine[j].nonce, 8, hipMemcpyHostToDevice), "write nonce");
+    check(hipIpcGetMemHandle(&mine[j].h, a[j]), "export");
+    mine[j].addr = (uint64_t)(uintptr_t)a[j];
   }
-  MPI_Send(e.data(), (int)(nbuf * sizeof(Export)), MPI_BYTE, 1, tag, MPI_COMM_WORLD);
+  check(hipDeviceSynchronize(), "sync");
+  all.resize((size_t)np * nbuf);
+  const int b = (int)(nbuf * sizeof(Export));
+  MPI_Allgather(mine.data(), b, MPI_BYTE, all.data(), b, MPI_BYTE, MPI_COMM_WORLD);
   return a;
 }
 
@@ -82,12 +88,12 @@ int main(int argc, char **argv) {
   int me = 0, np = 1;
   MPI_Comm_rank(MPI_COMM_WORLD, &me);
   MPI_Comm_size(MPI_COMM_WORLD, &np);
-  if (np != 2) {
-    if (me == 0) std::fprintf(stderr, "ipc_reuse: run with 2 ranks\n");
+  if (np < 2) {
+    if (me == 0) std::fprintf(stderr, "ipc_reuse: run with >= 2 ranks\n");
     MPI_Finalize();
     return 2;
   }
-  const int rounds = argc > 1 ? std::atoi(argv[1]) : 8;
+  const int rounds = argc > 1 ? std::atoi(argv[1]) : 6;
   int ndev = 0;
   check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
   check(hipSetDevice(me % ndev), "hipSetDevice");
@@ -97,56 +103,55 @@ int main(int argc, char **argv) {
   const int nbufs[2] = {1, 3};
   for (size_t bytes : sizes)
     for (int nbuf : nbufs)
-      for (const char *variant : {"close", "keep"}) {
-        const bool close_first = std::string(variant) == "close";
-        int same_addr = 0, first_ok = 0, copy_ok = 0, kernel_ok = 0, reads = 0;
-        std::vector<void *> kept;  // importer: mappings left open ("keep")
+      for (const char *variant : {"close", "keep", "mixed"}) {
+        const std::string v = variant;
+        const bool do_close = v == "close" || (v == "mixed" && me % 2 == 0);
+        long st[5] = {0, 0, 0, 0, 0};  // reads, first ok, recycled, copy ok, kernel ok
+        std::vector<void *> kept;
         for (int r = 0; r < rounds; r++) {
-          std::vector<void *> a;
-          std::vector<Export> e(nbuf), f(nbuf);
-          if (me == 0) {
-            a = owner_round(bytes, nbuf, 0);  // 1.
-          } else {  // 2.
-            MPI_Recv(e.data(), (int)(nbuf * sizeof(Export)), MPI_BYTE, 0, 0, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
-            std::vector<void *> m(nbuf);
-            for (int j = 0; j < nbuf; j++) {
-              check(hipIpcOpenMemHandle(&m[j], e[j].h, hipIpcMemLazyEnablePeerAccess), "open A");
-              if (read_views(m[j], e[j].nonce, scratch) == 3) first_ok++;
+          std::vector<Export> ea, eb;
+          std::vector<void *> a = alloc_and_export(bytes, nbuf, me, np, ea);  // 1.
+          std::vector<void *> ma;
+          for (int p = 0; p < np; p++)  // 2.
+            for (int j = 0; j < nbuf && p != me; j++) {
+              const Export &e = ea[(size_t)p * nbuf + j];
+              void *m = nullptr;
+              check(hipIpcOpenMemHandle(&m, e.h, hipIpcMemLazyEnablePeerAccess), "open A");
+              if (read_views(m, e.nonce, scratch) == 3) st[1]++;
+              ma.push_back(m);
             }
-            for (int j = 0; j < nbuf; j++) {
-              if (close_first) check(hipIpcCloseMemHandle(m[j]), "close A");
-              else kept.push_back(m[j]);
-            }
+          for (void *m : ma) {
+            if (do_close) check(hipIpcCloseMemHandle(m), "close A");
+            else kept.push_back(m);
           }
           MPI_Barrier(MPI_COMM_WORLD);
-          if (me == 0) {  // 3.
-            for (void *p : a) check(hipFree(p), "free A");
-            std::vector<void *> b = owner_round(bytes, nbuf, 1);
-            MPI_Barrier(MPI_COMM_WORLD);  // the importer has read B
-            for (void *p : b) check(hipFree(p), "free B");
-          } else {  // 4.
-            MPI_Recv(f.data(), (int)(nbuf * sizeof(Export)), MPI_BYTE, 0, 1, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
-            for (int j = 0; j < nbuf; j++) {
+          for (void *p : a) check(hipFree(p), "free A");  // 3.
+          std::vector<void *> b = alloc_and_export(bytes, nbuf, me, np, eb);
+          for (int p = 0; p < np; p++)  // 4.
+            for (int j = 0; j < nbuf && p != me; j++) {
+              const Export &f = eb[(size_t)p * nbuf + j];
               for (int i = 0; i < nbuf; i++)
-                if (f[j].addr == e[i].addr) same_addr++;
+                if (f.addr == ea[(size_t)p * nbuf + i].addr) st[2]++;
               void *m = nullptr;
-              check(hipIpcOpenMemHandle(&m, f[j].h, hipIpcMemLazyEnablePeerAccess), "open B");
-              const int v = read_views(m, f[j].nonce, scratch);
-              copy_ok += v & 1;
-              kernel_ok += (v >> 1) & 1;
-              reads++;
+              check(hipIpcOpenMemHandle(&m, f.h, hipIpcMemLazyEnablePeerAccess), "open B");
+              const int got = read_views(m, f.nonce, scratch);
+              st[0]++;
+              st[3] += got & 1;
+              st[4] += (got >> 1) & 1;
               check(hipIpcCloseMemHandle(m), "close B");
             }
-            MPI_Barrier(MPI_COMM_WORLD);
-          }
+          MPI_Barrier(MPI_COMM_WORLD);
+          for (void *p : b) check(hipFree(p), "free B");
           MPI_Barrier(MPI_COMM_WORLD);
         }
         for (void *m : kept) check(hipIpcCloseMemHandle(m), "close kept");
-        if (me == 1)
-          std::printf("{\"variant\": \"%s\", \"bytes\": %zu, \"buffers\": %d, \"rounds\": %d, \"devices\": %d, "
-                      "\"reads\": %d, \"first_mapping_ok\": %d, \"recycled_address\": %d, "
-                      "\"second_mapping_copy_engine_ok\": %d, \"second_mapping_kernel_ok\": %d}\n",
-                      variant, bytes, nbuf, rounds, ndev, reads, first_ok, same_addr, copy_ok, kernel_ok);
+        long tot[5];
+        MPI_Reduce(st, tot, 5, MPI_LONG, MPI_SUM, 0, MPI_COMM_WORLD);
+        if (me == 0)
+          std::printf("{\"variant\": \"%s\", \"ranks\": %d, \"bytes\": %zu, \"buffers\": %d, \"rounds\": %d, "
+                      "\"devices\": %d, \"reads\": %ld, \"first_mapping_ok\": %ld, \"recycled_address\": %ld, "
+                      "\"second_mapping_copy_engine_ok\": %ld, \"second_mapping_kernel_ok\": %ld}\n",
+                      variant, np, bytes, nbuf, rounds, ndev, tot[0], tot[1], tot[2], tot[3], tot[4]);
         std::fflush(stdout);
         MPI_Barrier(MPI_COMM_WORLD);
       }

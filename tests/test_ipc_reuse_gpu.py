@@ -1,12 +1,13 @@
 """GPU tier: the HIP IPC behaviour the transport's retired mappings rest on.
 
-tests/cpp/ipc_reuse.cpp (two MPI processes) runs, per round: the owner
-exports fresh allocations A, the importer opens them and either closes the
-mappings ("close") or keeps them ("keep"); the owner frees A, allocates B of
-the same sizes (usually at A's addresses) and exports them; the importer
-opens B and reads the owner's nonces through the copy engine and through a
-kernel.  Cases: 64 MiB (own allocations) and 1 MiB (sub-allocated) buffers,
-one or three per round.
+tests/cpp/ipc_reuse.cpp (2 or 4 MPI processes, all-to-all like a
+communicator) runs, per round: every rank exports fresh allocations A, every
+peer opens them and then closes its mappings ("close"), keeps them
+("keep") or -- "mixed" -- odd ranks keep and even ranks close; every rank
+frees A, allocates B of the same sizes (usually at A's addresses) and
+exports them; the peers open B and read the owner's nonces through the copy
+engine and through a kernel.  Cases: 64 MiB (own allocations) and 1 MiB
+(sub-allocated) buffers, one or three per rank.
 
 The design (include/hiccl/transport.h IpcMapping)
 retires mappings instead of closing them.  This test asserts that "keep"
@@ -28,14 +29,15 @@ MPIRUN = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
 EXE = os.path.join(ROOT, "build", "ipc_reuse")
 
 
-def test_ipc_close_then_reopen_recycled_address_outcome():
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_ipc_close_then_reopen_recycled_address_outcome(ranks):
     rounds = 6
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    p = subprocess.run(["timeout", "-k", "10", "120", MPIRUN, "-np", "2", EXE, str(rounds)],
+    p = subprocess.run(["timeout", "-k", "10", "150", MPIRUN, "-np", str(ranks), EXE, str(rounds)],
                        capture_output=True, text=True, env=env, cwd="/tmp")
     assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
     rows = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(rows) == 8, p.stdout
+    assert len(rows) == 12, p.stdout
     out = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, "ipc_reuse.jsonl"), "a") as f:
