@@ -970,14 +970,16 @@ def crossover(args):
 
 
 def progstep(args):
-    """One C5 pipeline step on one GPU, without peers: the step's element
+    """One C5 pipeline step on one GPU, without peers: the step's enqueue
     sequence -- a ready phase, the transport's copies (five 1 MiB byte
     copies), a done phase, the reductions (4 x n=2 + 1 x n=4 computes of
     2^18 f32, the {1,4,2} step shape), a tail phase --
-    as separate launches (k_sigwait_phases + plan kernels, the round-2
-    stream-ordered path) and as ONE step program; queued GPU time per step
-    (events around 200 back-to-back steps), interleaved rounds.  The phases
-    signal and await this process's own flags (always satisfied)."""
+    as separate launches (k_sigwait_phases + plan kernels: 5 kernels, the
+    round-2 stream-ordered path) and as programs (each phase folded into the
+    launch of the batch after it: 2 kernels + the tail phase, which in a
+    pipeline folds into the next step's first program); queued GPU time per
+    step (events around 200 back-to-back steps), interleaved rounds.  The
+    phases signal and await this process's own flags (always satisfied)."""
     c = 1 << 18
     dev = torch.cuda.current_device()
     bufs = [torch.empty(c, device="cuda") for _ in range(12)]
@@ -1013,46 +1015,38 @@ def progstep(args):
         comp.enqueue(stream)
         phase(f[2], epoch[0])
 
-    prog = hiccl_amd.Program(torch.float32, device=dev)
-    prog.add_signal([f[0]], [f[0]])
-    prog.add_plan(cp)
-    prog.add_signal([f[1]], [f[1]])
-    prog.add_plan(comp)
-    prog.add_signal([f[2]], [f[2]])
+    def build(phase_flag, plan):
+        pr = hiccl_amd.Program(torch.float32, device=dev)
+        if phase_flag is not None:
+            pr.add_signal([phase_flag], [phase_flag])
+        if plan is not None:
+            pr.add_plan(plan)
+        return pr
+
+    p_copy, p_comp, p_tail = build(f[0], cp), build(f[1], comp), build(f[2], None)
 
     def program():
         epoch[0] += 1
-        prog.launch([epoch[0]] * 3, err=err.data_ptr(), timeout_s=10.0, stream=stream)
+        for pr in (p_copy, p_comp, p_tail):
+            pr.launch([epoch[0]], err=err.data_ptr(), timeout_s=10.0, stream=stream)
+
+    def program_tail_folded():  # the tail phase rides in the next step's first program, as in a pipeline
+        epoch[0] += 1
+        p_copy.launch([epoch[0]], err=err.data_ptr(), timeout_s=10.0, stream=stream)
+        p_comp.launch([epoch[0]], err=err.data_ptr(), timeout_s=10.0, stream=stream)
 
     def separate_nophase():
         cp.enqueue(stream)
         comp.enqueue(stream)
 
-    prog2 = hiccl_amd.Program(torch.float32, device=dev)
-    prog2.add_plan(cp)
-    prog2.add_plan(comp)
+    q_copy, q_comp = build(None, cp), build(None, comp)
 
     def program_nophase():
-        prog2.launch(stream=stream)
+        q_copy.launch(stream=stream)
+        q_comp.launch(stream=stream)
 
-    runs = {"separate": separate, "program": program, "separate_no_phases": separate_nophase,
-            "program_no_phases": program_nophase}
-    # the program at fewer workgroups (fewer ticket / completion atomics)
-    progs_wg = []
-    for wg in (256, 128, 64):
-        pw = hiccl_amd.Program(torch.float32, device=dev)
-        pw.add_signal([f[0]], [f[0]])
-        pw.add_plan(cp)
-        pw.add_signal([f[1]], [f[1]])
-        pw.add_plan(comp)
-        pw.add_signal([f[2]], [f[2]])
-        pw.set_max_workgroups(wg)
-        progs_wg.append(pw)
-
-        def run_wg(pw=pw):
-            epoch[0] += 1
-            pw.launch([epoch[0]] * 3, err=err.data_ptr(), timeout_s=10.0, stream=stream)
-        runs[f"program_wg{wg}"] = run_wg
+    runs = {"separate": separate, "program": program, "program_tail_folded": program_tail_folded,
+            "separate_no_phases": separate_nophase, "program_no_phases": program_nophase}
     res = {k: [] for k in runs}
     for _ in range(5):
         for k, fn in runs.items():
@@ -1073,10 +1067,8 @@ def progstep(args):
         row[k + "_us"] = round(float(np.median(v)), 3)
     row["saved_us_per_step"] = round(row["separate_us"] - row["program_us"], 3)
     print(json.dumps(row), flush=True)
-    prog.close()
-    prog2.close()
-    for pw in progs_wg:
-        pw.close()
+    for pr in (p_copy, p_comp, p_tail, q_copy, q_comp):
+        pr.close()
     return 0
 
 

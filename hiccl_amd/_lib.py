@@ -105,9 +105,9 @@ _SIGS = {
     "hiccl_signal_wait_phases": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, ctypes.c_double, _vp]),
     "hiccl_program_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     "hiccl_program_add_signal": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp, ctypes.c_int]),
-    "hiccl_program_add_plan": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
+    "hiccl_program_add_plan": (ctypes.c_int, [_vp, _vp]),
     "hiccl_program_set_max_workgroups": (ctypes.c_int, [_vp, ctypes.c_int]),
-    "hiccl_program_num_segments": (ctypes.c_int, [_vp]),
+    "hiccl_program_num_units": (ctypes.c_int, [_vp]),
     "hiccl_program_num_phases": (ctypes.c_int, [_vp]),
     "hiccl_program_launch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_double, _vp]),
     "hiccl_program_destroy": (None, [_vp]),

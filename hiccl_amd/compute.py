@@ -240,15 +240,16 @@ class Compute:
 
 
 class Program:
-    """A step program (include/hiccl_reduce.h ``hiccl_program_*``): an ordered
-    list of signal/wait phases and plans' computes that runs as ONE kernel
-    launch, each element after the previous one completed -- the ordered work
-    of one stream-ordered pipeline step (what HiCCL::Comm records per step).
+    """A program (include/hiccl_reduce.h ``hiccl_program_*``): signal/wait
+    phases folded into the launch of one batch of independent computes --
+    the phases run first (one wave, in order), the units after the last
+    phase.  HiCCL::Comm records its stream-ordered pipeline as programs.
 
-    add_signal(sig_ptrs, wait_ptrs)   one phase (device flag addresses).
-    add_plan(compute, join=False)     the computes a :class:`Compute` holds now
-                                      (its dtype must be the program's, or
-                                      torch.uint8 = exact byte copies).
+    add_signal(sig_ptrs, wait_ptrs)   one phase (device flag addresses),
+                                      before the first add_plan.
+    add_plan(compute)                 the computes a :class:`Compute` holds
+                                      now (its dtype must be the program's,
+                                      or torch.uint8 = exact byte copies).
     launch(epochs, epoch_dev, err, timeout_s, stream)
     """
 
@@ -266,16 +267,16 @@ class Program:
         L.check(L.lib().hiccl_program_add_signal(self._prog, st, len(sig_ptrs), wt, len(wait_ptrs)),
                 "program_add_signal")
 
-    def add_plan(self, compute, join=False):
-        L.check(L.lib().hiccl_program_add_plan(self._prog, compute._plan, 1 if join else 0), "program_add_plan")
+    def add_plan(self, compute):
+        L.check(L.lib().hiccl_program_add_plan(self._prog, compute._plan), "program_add_plan")
         self._keep.append(compute)
 
     def set_max_workgroups(self, n):
-        """Cap the launch at ``n`` workgroups (0: 2 per CU)."""
+        """Cap the launch at ``n`` workgroups (0: the default)."""
         L.check(L.lib().hiccl_program_set_max_workgroups(self._prog, int(n)), "program_set_max_workgroups")
 
-    def segments(self):
-        return L.lib().hiccl_program_num_segments(self._prog)
+    def units(self):
+        return L.lib().hiccl_program_num_units(self._prog)
 
     def phases(self):
         return L.lib().hiccl_program_num_phases(self._prog)

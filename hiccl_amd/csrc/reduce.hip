@@ -738,90 +738,62 @@ __global__ __launch_bounds__(64) void k_counter_add(uint32_t *ctr, uint32_t v) {
 
 // ------------------------------------------------------------ step programs --
 //
-// A stream-ordered pipeline step is a short ordered list of work: signal /
-// wait phases (ready tokens), the transport's batched copies, more phases
-// (done tokens), the step's reductions, the fused transfers' done tokens.
-// Launched one by one that is four or five kernels per step, each boundary
-// ~1.5-1.9 us (MI355X_MICROARCH.md).  A step PROGRAM runs the whole list in
-// one launch: the list is a sequence of SEGMENTS (kind 1: signal/wait phases,
-// run by one wave as k_sigwait_phases does; kind 0: units -- tiles of a set of
-// computes, reductions in the program's type or exact byte copies), and the
-// grid works through TICKETS taken in order from a device counter.  Ticket k
-// belongs to segment s(k); before working on it a workgroup waits until
-// segment s(k) - 1 is complete.  Every ticket of an earlier segment was taken
-// before k by a workgroup that is running, so the wait always ends: unlike a
-// grid barrier this needs no co-residency of the grid.  Completions are
-// published once per workgroup and segment (release fence at system scope --
-// peers read what the copies and reductions wrote -- then an agent-scope
-// counter add); a workgroup that passes a gate takes a system-scope acquire,
-// so the peers' writes its signal/wait segment waited for are seen by every
-// XCD's L2.  Same stores and waits, in the same order, as the separate
-// launches; bits identical.
+// A stream-ordered pipeline step is a short ordered list: ready-token phases,
+// the transport's batched copies, done-token phases, the step's reductions,
+// the fused transfers' done tokens.  Launched one by one that is a
+// k_sigwait_phases before every copy or reduction kernel.  A PROGRAM folds
+// the signal/wait phases that precede a batch of units into that batch's
+// kernel as a PROLOGUE: workgroup 0's first wave runs the phases in order
+// (system-scope release stores of the epochs, bounded acquire spins -- as
+// k_sigwait_phases), then publishes the launch's sequence number in the
+// program's gate word; every other workgroup waits for that word before its
+// first unit.  The units are the tiles of the batch's computes (reductions in
+// the program's type, or exact byte copies), statically interleaved over the
+// grid like the plan kernel.
+//
+// Measured alternative (round 3, profiles/r03f_progstep_*.jsonl): running a
+// whole step -- several unit batches with completion gates between them --
+// in one launch.  Completions then need grid-wide counting (atomics on one
+// line from every workgroup) and, MI355X's L2 being per XCD, a system-scope
+// L2 writeback per workgroup before each count and an invalidate after each
+// gate: 40-170 us per step against 18-22 us for the separate launches.  A
+// kernel boundary does that cache maintenance once per XCD.  So units that
+// depend on other units stay in separate launches; only the token phases
+// move into the kernels.
+//
+// Coherence of the prologue: no unit of the launch touches its data before
+// the gate opens, so the data the phases waited for (peers' writes over
+// xGMI) is read after it arrived, as it is by a kernel launched after a
+// separate k_sigwait_phases; the launch's own stores are released at its
+// end like any kernel's.
 
-constexpr int kProgMaxSegs = 48;
 constexpr int kProgMaxPhases = 64;
 constexpr int kProgBlock = 256;
 constexpr int kProgPol = 11;  // nt loads, nt stores (the library's default policy)
-// Counters 256 B apart: the ticket counter's atomics must not share a line
-// with the completion counters that waiting workgroups poll.
-constexpr int kCtrStride = 64;  // uint32 words
-constexpr size_t kCtrBytes = (size_t)(2 + kProgMaxSegs) * kCtrStride * 4;
-
-struct ProgSeg {
-  uint32_t tick_begin;  // first ticket (segment s owns [tick_begin, seg[s+1].tick_begin))
-  uint32_t kind;        // 0: units, 1: signal/wait phases
-  uint32_t first;       // units: first unit; phases: first phase
-  uint32_t count;       // units: units; phases: phases
-  uint32_t grab;        // units per ticket (units segments)
-  uint32_t need;        // completions that close the segment (its units, or 1)
-};
 
 struct ProgPhase {
   uint32_t sig_begin, sig_end, wait_begin, wait_end;
 };
 
 struct ProgArgs {
-  const PlanDesc *desc;  // computes of every units segment; pad bit 0: exact byte copy
+  const PlanDesc *desc;  // computes of the unit batch; pad bit 0: exact byte copy
   const char *const *ptrs;
   const uint32_t *unit_comp;
   const ProgPhase *phase;
   uint32_t *const *sig;
   const uint32_t *const *wait;
-  uint32_t *ctr;  // [0] tickets, [1] exits, [2 + s] completions of segment s (x kCtrStride); zero between launches
+  uint32_t *gate;  // workgroup 0 stores the launch's sequence number here after the phases
   uint32_t *err;
   const uint32_t *epoch_dev;
   uint64_t timeout_ticks;
-  uint32_t stride, nseg, nticket, nphase;
-  uint32_t fences;  // measurement only (HICCL_PROGRAM_FENCES): bit 0 skips the release, bit 1 the acquire fences
-  uint32_t pad;
-  ProgSeg seg[kProgMaxSegs];
+  uint64_t nunits;
+  uint32_t stride, nphase, seq, pad;
   uint32_t epoch[kProgMaxPhases];  // per launch: phase p stores / awaits epoch[p] (+ *epoch_dev)
 };
 
-// Bounded spin of one lane until *c >= need: false on time-out or an error
-// recorded by anyone (then *err is set and the caller goes on without
-// waiting, so the grid always drains).
-// The poll is a RELAXED load: an acquire load invalidates the XCD's L2 on
-// every poll (buffer_inv sc1), and hundreds of waiting workgroups doing that
-// starve the ones at work; the caller takes one acquire fence after the wait.
-__device__ __forceinline__ void prog_gate_wait(const ProgArgs &a, const uint32_t *c, uint32_t need) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint32_t nap = 1;  // backoff: fewer polls of one line from hundreds of waiting workgroups
-  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-    for (uint32_t i = 0; i < nap; i++) __builtin_amdgcn_s_sleep(2);
-    if (nap < 16) nap <<= 1;
-    if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-      if (a.err) __hip_atomic_store(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
-    }
-  }
-}
-
-// Phases [first, first + count) on one wave (lanes = flags), as k_sigwait_phases.
-__device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t first, uint32_t count, uint32_t lane,
-                                            uint32_t add) {
-  for (uint32_t p = first; p < first + count; p++) {
+// Phases [0, count) on one wave (lanes = flags), as k_sigwait_phases.
+__device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t count, uint32_t lane, uint32_t add) {
+  for (uint32_t p = 0; p < count; p++) {
     const ConstU32 *q = (const ConstU32 *)&a.phase[p];
     const uint32_t s0 = q[0], s1 = q[1], w0 = q[2], w1 = q[3];
     const uint32_t epoch = a.epoch[p] + add;
@@ -847,6 +819,24 @@ __device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t first, u
   }
 }
 
+// Bounded wait of one lane until the gate word reaches `seq` (wrap-aware);
+// on a time-out or an error recorded by anyone it gives up (the grid drains,
+// the host reports the error).  Relaxed polls with backoff: hundreds of
+// workgroups poll one line.
+__device__ __forceinline__ void prog_gate_wait(const ProgArgs &a, uint32_t seq) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t nap = 1;
+  while ((int32_t)(__hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
+    for (uint32_t i = 0; i < nap; i++) __builtin_amdgcn_s_sleep(2);
+    if (nap < 8) nap <<= 1;
+    if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+      if (a.err) __hip_atomic_store(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
+}
+
 template <class Op, int U>
 __device__ __forceinline__ void prog_unit_of(const PlanDesc &d, TableInputs raw, uint64_t lt, int tid,
                                              const uint32_t (&voff)[U]) {
@@ -867,72 +857,29 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
   uint32_t voff[U];
 #pragma unroll
   for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * kProgBlock + tid) * kPacket);
-  __shared__ uint32_t s_tick[2];
-  const uint32_t add = a.epoch_dev ? __hip_atomic_load(a.epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-  if (tid == 0) s_tick[0] = __hip_atomic_fetch_add(&a.ctr[0 * kCtrStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  uint32_t k = __builtin_amdgcn_readfirstlane(s_tick[0]);  // workgroup-uniform: scalar from here on
-  int slot = 0;
-  uint32_t open = 0;               // segments below `open` are complete, as this workgroup has seen
-  uint32_t pend_seg = 0, pend = 0;  // completions of pend_seg done here, not yet published
-  auto publish = [&]() {
-    if (!(a.fences & 1u)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this wave's stores done, written back
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&a.ctr[(2 + pend_seg) * kCtrStride], pend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    pend = 0;
-  };
-  while (k < a.nticket) {
-    uint32_t s = 0;  // the segment of ticket k (kernarg: scalar loads)
-    while (s + 1 < a.nseg && a.seg[s + 1].tick_begin <= k) s++;
-    // the next ticket, taken before this one's work (its latency hides under it)
-    uint32_t nxt = 0;
-    if (tid == 0) nxt = __hip_atomic_fetch_add(&a.ctr[0 * kCtrStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (pend && pend_seg != s) publish();  // before any wait: others may be waiting for it
-    if (s > open) {
-      if (tid == 0) prog_gate_wait(a, &a.ctr[(2 + s - 1) * kCtrStride], a.seg[s - 1].need);
-      __syncthreads();
-      if (!(a.fences & 2u)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // see what they (and peers) wrote
-      open = s;
-    }
-    const uint32_t kind = a.seg[s].kind, first = a.seg[s].first, count = a.seg[s].count;
-    if (kind == 1) {
-      if (tid < 64) prog_phases(a, first, count, (uint32_t)tid, add);
-      pend_seg = s;
-      pend = 1;
-    } else {
-      const uint32_t grab = a.seg[s].grab;
-      const uint32_t u0 = first + (k - a.seg[s].tick_begin) * grab;
-      const uint32_t u1 = u0 + grab < first + count ? u0 + grab : first + count;
-      for (uint32_t t = u0; t < u1; t++) {
-        const uint32_t c = a.unit_comp ? ((ConstU32 *)a.unit_comp)[t] : 0u;
-        const ConstDesc *q = (const ConstDesc *)a.desc + c;
-        const PlanDesc d = load_desc(a.desc, c);
-        const bool bytes = (q->pad & 1u) != 0;
-        TableInputs raw{a.ptrs + (uint64_t)c * a.stride};
-        if (bytes)
-          prog_unit_of<OpRaw, U>(d, raw, t - d.tile_begin, tid, voff);
-        else
-          prog_unit_of<Op, U>(d, raw, t - d.tile_begin, tid, voff);
+  if (a.nphase) {
+    const uint32_t add = a.epoch_dev ? __hip_atomic_load(a.epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const uint32_t seq = a.seq + add;
+    if (blockIdx.x == 0) {
+      if (tid < 64) {
+        prog_phases(a, a.nphase, (uint32_t)tid, add);
+        if (tid == 0) __hip_atomic_store(a.gate, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
-      pend_seg = s;
-      pend += u1 - u0;
+    } else if (tid == 0) {
+      prog_gate_wait(a, seq);
     }
-    if (tid == 0) s_tick[slot ^ 1] = nxt;
     __syncthreads();
-    slot ^= 1;
-    k = __builtin_amdgcn_readfirstlane(s_tick[slot]);
   }
-  if (pend) publish();
-  if (tid == 0) {
-    // every ticket take of this workgroup precedes its exit increment; the
-    // last one out leaves the counters zero for the next launch
-    const uint32_t prev = __hip_atomic_fetch_add(&a.ctr[1 * kCtrStride], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      __hip_atomic_store(&a.ctr[0 * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&a.ctr[1 * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (uint32_t s = 0; s < a.nseg; s++)
-        __hip_atomic_store(&a.ctr[(2 + s) * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+  for (uint64_t t = blockIdx.x; t < a.nunits; t += gridDim.x) {
+    const uint32_t c = a.unit_comp ? ((ConstU32 *)a.unit_comp)[t] : 0u;
+    const ConstDesc *q = (const ConstDesc *)a.desc + c;
+    const PlanDesc d = load_desc(a.desc, c);
+    const bool bytes = (q->pad & 1u) != 0;
+    TableInputs raw{a.ptrs + (uint64_t)c * a.stride};
+    if (bytes)
+      prog_unit_of<OpRaw, U>(d, raw, t - d.tile_begin, tid, voff);
+    else
+      prog_unit_of<Op, U>(d, raw, t - d.tile_begin, tid, voff);
   }
 }
 
@@ -2102,31 +2049,30 @@ struct hiccl_program {
     size_t count;
     bool bytes;  // exact byte copy (a HICCL_BYTES plan's compute)
   };
-  struct Seg {
-    int kind;  // 0 units, 1 signal/wait phases
-    std::vector<Unit> units;
-    uint32_t phase0, nphase;
-  };
-  std::vector<Seg> segs;
+  std::vector<Unit> units;  // the unit batch (after the phases)
   struct Phase {
     std::vector<uint32_t *> sig;
     std::vector<const uint32_t *> wait;
   };
-  std::vector<Phase> phases;
+  std::vector<Phase> phases;  // the prologue
   bool dirty = true;
   char *d_block = nullptr;
-  uint32_t *d_ctr = nullptr;
+  uint32_t *d_gate = nullptr;
+  uint32_t seq = 0;  // last sequence number used (eager launches; captures reserve a range)
   ProgArgs args;
   int unroll = 4;
   uint32_t grid = 0;
-  uint32_t max_wg = 0;  // hiccl_program_set_max_workgroups (0: CUs x kProgBpc)
+  uint32_t max_wg = 0;  // hiccl_program_set_max_workgroups (0: default)
   std::atomic<bool> enqueued{false};
 };
 
 namespace {
 
-constexpr int kProgBpc = 2;           // workgroups per CU of a program launch
-constexpr uint32_t kProgTicketsPerWG = 16;  // units segments: about this many tickets per workgroup at most
+// Workgroups per CU of a program launch: a small batch (under one 16 KiB
+// tile per lane-group per CU, the C5 step) takes 4 like the plan kernel's
+// small launches, larger ones 2.
+constexpr int kProgSmallBpc = 4;
+constexpr int kProgBpc = 2;
 
 typedef void (*prog_fn)(const ProgArgs &, dim3, hipStream_t);
 
@@ -2165,79 +2111,53 @@ int prog_upload(hiccl_program *p, hipStream_t s) {
     (void)hipFree(p->d_block);
     p->d_block = nullptr;
   }
-  if (!p->d_ctr) {
-    if (int e = check_hip(hipMalloc((void **)&p->d_ctr, kCtrBytes), "program: hipMalloc(counters)")) return e;
-    if (int e = check_hip(hipMemset(p->d_ctr, 0, kCtrBytes), "program: hipMemset(counters)")) return e;
+  if (!p->d_gate) {
+    if (int e = check_hip(hipMalloc((void **)&p->d_gate, 256), "program: hipMalloc(gate)")) return e;
+    if (int e = check_hip(hipMemset(p->d_gate, 0, 256), "program: hipMemset(gate)")) return e;
+    p->seq = 0;
   }
   const int cus = device_cus(p->device);
   const size_t tesz = esize(p->dtype);
   auto esz_of = [&](const hiccl_program::Unit &u) { return u.bytes ? (size_t)1 : tesz; };
-  // one tile shape for the launch: half-size tiles when the whole program
-  // has under two 16 KiB tiles per CU (auto_unroll; the C5 step)
   uint64_t total_pkt = 0;
-  size_t ncomp = 0, maxn = 1;
-  for (auto &g : p->segs)
-    for (auto &u : g.units) {
-      total_pkt += split_on(u.out, u.count, esz_of(u)).npkt;
-      ncomp++;
-      if (u.in.size() > maxn) maxn = u.in.size();
-    }
-  p->unroll = pick_prog(p->dtype, 2) && total_pkt < 2ull * cus * kProgBlock * 4 ? 2 : 4;
+  size_t maxn = 1;
+  for (auto &u : p->units) {
+    total_pkt += split_on(u.out, u.count, esz_of(u)).npkt;
+    if (u.in.size() > maxn) maxn = u.in.size();
+  }
+  // half-size tiles when the batch has under two 16 KiB tiles per CU (auto_unroll)
+  const bool small = total_pkt < 2ull * cus * kProgBlock * 4;
+  p->unroll = pick_prog(p->dtype, 2) && small ? 2 : 4;
   const uint64_t unit = (uint64_t)kProgBlock * p->unroll;
-  // the units of every segment, in order, and the ticket layout
-  uint32_t grid_cap = (uint32_t)(cus * kProgBpc);
-  if (p->max_wg && p->max_wg < grid_cap) grid_cap = p->max_wg;
+  const size_t ncomp = p->units.size();
   std::vector<uint32_t> unit_comp;
   std::vector<PlanDesc> desc(ncomp);
   std::vector<const void *> ptrs(ncomp * maxn, nullptr);
+  for (size_t c = 0; c < ncomp; c++) {
+    auto &u = p->units[c];
+    const Split sp = split_on(u.out, u.count, esz_of(u));
+    PlanDesc &d = desc[c];
+    d.out = (char *)u.out;
+    d.npkt = sp.npkt;
+    d.head = sp.head;
+    d.tail = sp.tail;
+    d.n = (uint32_t)u.in.size();
+    d.pad = u.bytes ? 1u : 0u;
+    d.tile_begin = unit_comp.size();
+    for (size_t k = 0; k < u.in.size(); k++) ptrs[c * maxn + k] = u.in[k];
+    const uint64_t nt = tiles_for(sp.npkt, unit);
+    for (uint64_t t = 0; t < nt; t++) unit_comp.push_back((uint32_t)c);
+  }
+  if (unit_comp.size() > 0xffffffffull) return fail(hipErrorInvalidValue, "program: more than 2^32 tiles");
   ProgArgs &a = p->args;
   memset(&a, 0, sizeof(a));
-  uint64_t tickets = 0;
-  size_t c = 0;
-  for (size_t si = 0; si < p->segs.size(); si++) {
-    auto &g = p->segs[si];
-    ProgSeg &ps = a.seg[si];
-    ps.tick_begin = (uint32_t)tickets;
-    ps.kind = (uint32_t)g.kind;
-    if (g.kind == 1) {
-      ps.first = g.phase0;
-      ps.count = g.nphase;
-      ps.grab = 1;
-      ps.need = 1;
-      tickets += 1;
-      continue;
-    }
-    ps.first = (uint32_t)unit_comp.size();
-    for (auto &u : g.units) {
-      const Split sp = split_on(u.out, u.count, esz_of(u));
-      PlanDesc &d = desc[c];
-      d.out = (char *)u.out;
-      d.npkt = sp.npkt;
-      d.head = sp.head;
-      d.tail = sp.tail;
-      d.n = (uint32_t)u.in.size();
-      d.pad = u.bytes ? 1u : 0u;
-      d.tile_begin = unit_comp.size();
-      for (size_t k = 0; k < u.in.size(); k++) ptrs[c * maxn + k] = u.in[k];
-      const uint64_t nt = tiles_for(sp.npkt, unit);
-      for (uint64_t t = 0; t < nt; t++) unit_comp.push_back((uint32_t)c);
-      c++;
-    }
-    const uint64_t units = unit_comp.size() - ps.first;
-    if (units > 0xffffffffull || unit_comp.size() > 0xffffffffull)
-      return fail(hipErrorInvalidValue, "program: more than 2^32 tiles");
-    ps.count = (uint32_t)units;
-    const uint64_t per = (uint64_t)grid_cap * kProgTicketsPerWG;
-    ps.grab = (uint32_t)(units > per ? (units + per - 1) / per : 1);
-    ps.need = (uint32_t)units;
-    tickets += (units + ps.grab - 1) / ps.grab;
-  }
-  if (tickets > 0xffffffffull) return fail(hipErrorInvalidValue, "program: too many tickets");
-  a.nseg = (uint32_t)p->segs.size();
-  a.nticket = (uint32_t)tickets;
+  a.nunits = unit_comp.size();
   a.nphase = (uint32_t)p->phases.size();
   a.stride = (uint32_t)maxn;
-  p->grid = (uint32_t)(tickets < grid_cap ? tickets : grid_cap);
+  uint64_t grid = (uint64_t)cus * (small ? kProgSmallBpc : kProgBpc);
+  if (p->max_wg && p->max_wg < grid) grid = p->max_wg;
+  if (grid > a.nunits) grid = a.nunits;
+  p->grid = (uint32_t)(grid ? grid : 1);  // a phases-only program: workgroup 0 alone
   // device block: [desc | ptrs | unit_comp | phases | sig | wait]
   size_t nsig = 0, nwait = 0;
   for (auto &ph : p->phases) {
@@ -2275,11 +2195,11 @@ int prog_upload(hiccl_program *p, hipStream_t s) {
     return e;
   a.desc = (const PlanDesc *)(p->d_block + o_desc);
   a.ptrs = (const char *const *)(p->d_block + o_ptrs);
-  a.unit_comp = (const uint32_t *)(p->d_block + o_uc);
+  a.unit_comp = ncomp > 1 ? (const uint32_t *)(p->d_block + o_uc) : nullptr;
   a.phase = (const ProgPhase *)(p->d_block + o_ph);
   a.sig = (uint32_t *const *)(p->d_block + o_sig);
   a.wait = (const uint32_t *const *)(p->d_block + o_wait);
-  a.ctr = p->d_ctr;
+  a.gate = p->d_gate;
   p->dirty = false;
   return 0;
 }
@@ -2311,37 +2231,26 @@ int hiccl_program_add_signal(hiccl_program_t *p, uint32_t *const *sig, int nsig,
     if (!sig[i]) return fail(hipErrorInvalidValue, "program_add_signal: NULL signal flag");
   for (int i = 0; i < nwait; i++)
     if (!wait[i]) return fail(hipErrorInvalidValue, "program_add_signal: NULL wait flag");
+  if (!p->units.empty())
+    return fail(hipErrorInvalidValue, "program_add_signal: phases precede the program's units (start a new program)");
   if (p->phases.size() >= (size_t)kProgMaxPhases)
     return fail(hipErrorInvalidValue, "program_add_signal: more than 64 phases in one program");
-  // consecutive phases share one segment (one wave runs them in order)
-  if (p->segs.empty() || p->segs.back().kind != 1) {
-    if (p->segs.size() >= (size_t)kProgMaxSegs)
-      return fail(hipErrorInvalidValue, "program_add_signal: more than 48 segments in one program");
-    p->segs.push_back(hiccl_program::Seg{1, {}, (uint32_t)p->phases.size(), 0});
-  }
   hiccl_program::Phase ph;
   ph.sig.assign(sig, sig + nsig);
   ph.wait.assign(wait, wait + nwait);
   p->phases.push_back(std::move(ph));
-  p->segs.back().nphase++;
   p->dirty = true;
   return 0;
 }
 
-int hiccl_program_add_plan(hiccl_program_t *p, const hiccl_reduce_plan_t *plan, int join) {
+int hiccl_program_add_plan(hiccl_program_t *p, const hiccl_reduce_plan_t *plan) {
   if (!p || !plan) return fail(hipErrorInvalidValue, "program_add_plan: NULL argument");
   const bool bytes = plan->dtype == HICCL_BYTES;
   if (!bytes && plan->dtype != p->dtype)
     return fail(hipErrorInvalidValue, "program_add_plan: the plan's dtype is neither the program's nor HICCL_BYTES");
   if (plan->req.acc == HICCL_ACC_WIDE)
     return fail(hipErrorInvalidValue, "program_add_plan: programs accumulate natively (HICCL_ACC_NATIVE) only");
-  if (plan->comps.empty()) return 0;
-  if (!join || p->segs.empty() || p->segs.back().kind != 0) {
-    if (p->segs.size() >= (size_t)kProgMaxSegs)
-      return fail(hipErrorInvalidValue, "program_add_plan: more than 48 segments in one program");
-    p->segs.push_back(hiccl_program::Seg{0, {}, 0, 0});
-  }
-  for (auto &c : plan->comps) p->segs.back().units.push_back(hiccl_program::Unit{c.out, c.in, c.count, bytes});
+  for (auto &c : plan->comps) p->units.push_back(hiccl_program::Unit{c.out, c.in, c.count, bytes});
   p->dirty = true;
   return 0;
 }
@@ -2354,7 +2263,7 @@ int hiccl_program_set_max_workgroups(hiccl_program_t *p, int max_wg) {
   return 0;
 }
 
-int hiccl_program_num_segments(const hiccl_program_t *p) { return p ? (int)p->segs.size() : 0; }
+int hiccl_program_num_units(const hiccl_program_t *p) { return p ? (int)p->units.size() : 0; }
 int hiccl_program_num_phases(const hiccl_program_t *p) { return p ? (int)p->phases.size() : 0; }
 
 int hiccl_program_launch(hiccl_program_t *p, const uint32_t *epochs, const uint32_t *epoch_dev, uint32_t *err,
@@ -2362,10 +2271,9 @@ int hiccl_program_launch(hiccl_program_t *p, const uint32_t *epochs, const uint3
   if (!p) return fail(hipErrorInvalidValue, "program_launch: prog is NULL");
   if (!p->phases.empty() && !epochs) return fail(hipErrorInvalidValue, "program_launch: epochs is NULL");
   if (int e = check_hip(hipSetDevice(p->device), "program_launch: hipSetDevice")) return e;
-  if (p->segs.empty()) return 0;
+  if (p->phases.empty() && p->units.empty()) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (int e = prog_upload(p, s)) return e;
-  if (p->args.nticket == 0) return 0;
   prog_fn fn = pick_prog(p->dtype, p->unroll);
   if (!fn) return fail(hipErrorInvalidValue, "program_launch: no kernel for this dtype / shape");
   ProgArgs a = p->args;
@@ -2373,11 +2281,10 @@ int hiccl_program_launch(hiccl_program_t *p, const uint32_t *epochs, const uint3
   a.epoch_dev = epoch_dev;
   a.timeout_ticks = (uint64_t)((timeout_s > 0 ? timeout_s : 30.0) * 1e8);  // s_memrealtime: 100 MHz
   for (uint32_t i = 0; i < a.nphase; i++) a.epoch[i] = epochs[i];
-  static const uint32_t fences = [] {
-    const char *e = getenv("HICCL_PROGRAM_FENCES");  // measurement only: see ProgArgs::fences
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
-  a.fences = fences;
+  // the gate's sequence number: one per eager launch; a captured launch
+  // uses seq + *epoch_dev (replay r: seq + r) and reserves 2^24 of them
+  a.seq = ++p->seq;
+  if (epoch_dev) p->seq += (1u << 24);
   fn(a, dim3(p->grid), s);
   p->enqueued.store(true, std::memory_order_relaxed);
   return check_hip(hipGetLastError(), "program_launch: launch");
@@ -2388,7 +2295,7 @@ void hiccl_program_destroy(hiccl_program_t *p) {
   (void)hipSetDevice(p->device);
   prog_quiesce(p);
   if (p->d_block) (void)hipFree(p->d_block);
-  if (p->d_ctr) (void)hipFree(p->d_ctr);
+  if (p->d_gate) (void)hipFree(p->d_gate);
   delete p;
 }
 

@@ -455,70 +455,75 @@ class Comm {
   }
 
   void enqueue_pipeline(hipStream_t s) {
+    if (programs) return enqueue_programs(s);
     const size_t nl = command_batch.size();
     std::vector<typename std::list<Command<T>>::iterator> it(nl);
     for (size_t i = 0; i < nl; i++) it[i] = command_batch[i].begin();
-    size_t step = 0;
     while (it[0] != command_batch[0].end()) {
-      if (programs) {
-        launch_step_program(step, it, s);
-      } else {
-        for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
-        for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
-        for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue_tail(s);
+      for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
+      for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
+      for (size_t i = 0; i < nl; i++) {
+        it[i]->comm->enqueue_tail(s);
+        ++it[i];
       }
-      for (size_t i = 0; i < nl; i++) ++it[i];
-      step++;
     }
     CommBench::flush_signals();  // (the last step's done tokens)
   }
 
-  // Step programs (HICCL_STEP_PROGRAM, on by default in stream-ordered mode):
-  // each pipeline step -- every library's ready tokens, copies and done
-  // tokens, the computes in reverse library order, the fused transfers' done
-  // tokens, i.e. the enqueue order above -- is recorded once (the first
-  // eager run) into a hiccl_program and from then on runs as ONE kernel
-  // launch per step (hiccl_program_launch; reference: comm.h:195-204's
-  // transport wait -> compute start -> compute wait, one boundary per call).
-  // The phases' epochs are read from their transports at each launch.
-  struct StepProgram {
-    hiccl_program_t *prog = nullptr;
-    std::vector<std::function<uint32_t()>> epoch_of;
-  };
-  std::vector<StepProgram> step_programs;
+  // Programs (HICCL_STEP_PROGRAM, on by default in stream-ordered mode): the
+  // first stream-ordered run() records the enqueue sequence above -- per
+  // step every library's ready tokens, copies and done tokens, the computes
+  // in reverse library order, the fused transfers' done tokens -- as a list
+  // of hiccl_programs, each a group of token phases folded into the launch
+  // of the copy or compute batch that follows it (include/hiccl_reduce.h);
+  // later runs launch the list: no separate signal/wait kernels (reference
+  // order: comm.h:195-204's transport wait -> compute start -> compute
+  // wait).  Every transport still counts the run (advance()), and each
+  // phase's epoch is read from its transport at launch.
+  std::vector<CommBench::StepRecorder::Launch> prog_launches;
+  bool prog_recorded = false;
   bool programs = false;
   bool in_capture = false;
 
-  template <class It>
-  void launch_step_program(size_t step, It &it, hipStream_t s) {
-    const size_t nl = command_batch.size();
-    if (step >= step_programs.size()) {  // record (never inside a capture: the first run is eager)
-      if (in_capture) CommBench::die("step program", "a step was first met inside a graph capture");
+  void enqueue_programs(hipStream_t s) {
+    if (!prog_recorded) {  // never inside a capture: the first run is eager
+      if (in_capture) CommBench::die("program", "the pipeline was first met inside a graph capture");
       CommBench::flush_signals();
       CommBench::StepRecorder rec;
-      if (hiccl_program_create(&rec.prog, dtype_of<T>(), CommBench::mydevice))
-        CommBench::die("step program", hiccl_last_error());
-      // A program's workgroups wait for their predecessors on the GPU; ranks
-      // sharing it (single-GPU rehearsals only) split its workgroup slots so
-      // every rank's program stays resident while the others wait for it.
-      if (device_ranks > 1 && hiccl_program_set_max_workgroups(rec.prog, program_grid_share()))
-        CommBench::die("step program", hiccl_last_error());
+      rec.dtype = dtype_of<T>();
+      rec.device = CommBench::mydevice;
+      // a program's workgroups wait on the GPU for its phases; ranks sharing
+      // the GPU (single-GPU rehearsals only) split its workgroup slots so
+      // every rank's kernels stay resident while the others wait for them
+      rec.max_wg = device_ranks > 1 ? program_grid_share() : 0;
       CommBench::step_recorder() = &rec;
-      for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
-      for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
-      for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue_tail(s);
+      const size_t nl = command_batch.size();
+      std::vector<typename std::list<Command<T>>::iterator> it(nl);
+      for (size_t i = 0; i < nl; i++) it[i] = command_batch[i].begin();
+      while (it[0] != command_batch[0].end()) {
+        for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
+        for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
+        for (size_t i = 0; i < nl; i++) {
+          it[i]->comm->enqueue_tail(s);
+          ++it[i];
+        }
+      }
       CommBench::flush_signals();
+      rec.close();
       CommBench::step_recorder() = nullptr;
-      step_programs.push_back(StepProgram{rec.prog, std::move(rec.epoch_of)});
+      prog_launches = std::move(rec.launches);
+      prog_recorded = true;
     } else {
-      for (size_t i = 0; i < nl; i++) it[i]->comm->advance();  // the execution counts, as enqueue() would
+      for_each_comm([](CommBench::Comm<T> &c) { c.advance(); });  // the run counts, as enqueue() would
     }
-    StepProgram &sp = step_programs[step];
-    std::vector<uint32_t> epochs(sp.epoch_of.size());
-    for (size_t i = 0; i < epochs.size(); i++) epochs[i] = sp.epoch_of[i]();
-    if (hiccl_program_launch(sp.prog, epochs.data(), in_capture ? graph_ctr : nullptr, flags.err, CommBench::signal_timeout(),
-                             s))
-      CommBench::die("step program", hiccl_last_error());
+    std::vector<uint32_t> epochs;
+    for (auto &L : prog_launches) {
+      epochs.resize(L.epoch_of.size());
+      for (size_t i = 0; i < epochs.size(); i++) epochs[i] = L.epoch_of[i]();
+      if (hiccl_program_launch(L.prog, epochs.data(), in_capture ? graph_ctr : nullptr, flags.err,
+                               CommBench::signal_timeout(), s))
+        CommBench::die("program", hiccl_last_error());
+    }
   }
 
   int program_grid_share() const {
@@ -606,8 +611,8 @@ class Comm {
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph_ctr) (void)hipFree(graph_ctr);
     if (!owned.empty() || !command_batch.empty()) (void)hipDeviceSynchronize();
-    for (auto &sp : step_programs) hiccl_program_destroy(sp.prog);
-    step_programs.clear();
+    for (auto &L : prog_launches) hiccl_program_destroy(L.prog);
+    prog_launches.clear();
 #endif
     // the steps' transports (releasing their IPC mappings) and computes (the
     // reference never deletes them)

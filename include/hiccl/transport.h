@@ -729,32 +729,58 @@ inline PendingSignals &pending_signals() {
   return p;
 }
 
-// Step programs (HiCCL::Comm, stream-ordered mode; hiccl_program_*): while a
+// Programs (HiCCL::Comm, stream-ordered mode; hiccl_program_*): while a
 // recorder is set on this thread, flush_signals() and the transport's and
-// computes' plan launches APPEND to the recorder's program instead of
-// enqueueing -- the step's whole ordered work then goes out as one launch.
-// A phase's epoch is not fixed in the program: epoch_of[p]() gives it at
-// each launch (the owning transport's current epoch).
+// computes' plan launches APPEND to the recorder instead of enqueueing.  The
+// recorder folds every group of queued phases into the program of the unit
+// batch that follows it (one launch: phases, then units), so a pipeline
+// becomes a list of programs with no separate signal/wait launches.  A
+// phase's epoch is not fixed in the program: epoch_of[p]() gives it at each
+// launch (the owning transport's current epoch).
 struct StepRecorder {
-  hiccl_program_t *prog = nullptr;
-  std::vector<std::function<uint32_t()>> epoch_of;
-  int last = 0;                   // kind of the last element appended: 0 phases, 1 copies, 2 computes
+  struct Launch {
+    hiccl_program_t *prog;
+    std::vector<std::function<uint32_t()>> epoch_of;
+  };
+  std::vector<Launch> launches;  // finished programs, in stream order
+  int dtype = 0, device = 0, max_wg = 0;
+  hiccl_program_t *cur = nullptr;
+  std::vector<std::function<uint32_t()>> cur_epochs;
+  bool cur_units = false;
+  int last = 0;                      // kind of the last batch appended: 1 copies, 2 computes
   const void *last_owner = nullptr;  // the transport whose copies were appended last
+
+  void open() {
+    if (cur) return;
+    if (hiccl_program_create(&cur, dtype, device)) die("program", hiccl_last_error());
+    if (max_wg && hiccl_program_set_max_workgroups(cur, max_wg)) die("program", hiccl_last_error());
+  }
+  void close() {
+    if (!cur) return;
+    launches.push_back(Launch{cur, std::move(cur_epochs)});
+    cur = nullptr;
+    cur_epochs.clear();
+    cur_units = false;
+    last = 0;
+  }
 };
 inline StepRecorder *&step_recorder() {
   static thread_local StepRecorder *r = nullptr;
   return r;
 }
 
-// Append plan `p` to the recording program: copies of one transport's
-// execution (move + self plans) share an element, so do the computes of a
-// step (the reference starts them together on separate streams,
-// comm.h:198-202, so they are independent); anything else starts after the
-// previous element.
+// Append plan `p` to the recording: copies of one transport's execution
+// (move + self plans) share a batch, so do the computes of a step (the
+// reference starts them together on separate streams, comm.h:198-202, so
+// they are independent); anything else starts a new program, i.e. runs
+// after the previous batch has completed (a kernel boundary).
 inline void record_plan(hiccl_reduce_plan_t *p, int kind, const void *owner) {
   StepRecorder *r = step_recorder();
-  const bool join = r->last == kind && (kind == 2 || r->last_owner == owner);
-  if (hiccl_program_add_plan(r->prog, p, join ? 1 : 0)) die("step program", hiccl_last_error());
+  const bool join = r->cur_units && r->last == kind && (kind == 2 || r->last_owner == owner);
+  if (r->cur_units && !join) r->close();
+  r->open();
+  if (hiccl_program_add_plan(r->cur, p)) die("program", hiccl_last_error());
+  r->cur_units = true;
   r->last = kind;
   r->last_owner = owner;
 }
@@ -763,13 +789,18 @@ inline void flush_signals() {
   PendingSignals &p = pending_signals();
   if (p.phases.empty()) return;
   if (StepRecorder *r = step_recorder()) {
+    if (r->cur_units) r->close();  // these phases guard the NEXT batch
     for (auto &ph : p.phases) {
-      if (hiccl_program_add_signal(r->prog, ph.sig.data(), (int)ph.sig.size(),
+      r->open();
+      if (hiccl_program_num_phases(r->cur) >= 64) {  // a program holds 64 phases: the rest go first in the next
+        r->close();
+        r->open();
+      }
+      if (hiccl_program_add_signal(r->cur, ph.sig.data(), (int)ph.sig.size(),
                                    (const uint32_t *const *)ph.wait.data(), (int)ph.wait.size()))
-        die("step program", hiccl_last_error());
-      r->epoch_of.push_back(ph.epoch_now);
+        die("program", hiccl_last_error());
+      r->cur_epochs.push_back(ph.epoch_now);
     }
-    r->last = 0;
     p.phases.clear();
     return;
   }

@@ -285,41 +285,42 @@ int hiccl_signal_wait_phases(const hiccl_signal_phase_t *phases, int nphases, co
                              uint32_t *err, double timeout_s, void *stream);
 
 /* ----------------------------------------------------------------------
- * Step programs: one launch per pipeline step (stream-ordered transport).
+ * Programs: token phases folded into the kernel of the work they guard
+ * (stream-ordered transport).
  *
  * The reference runs a step as transport start -> transport wait -> compute
- * start -> compute wait (comm.h:195-204), i.e. separate launches and host
- * synchronisations per step.  A program is the ordered work of one step --
- * signal/wait phases (as hiccl_signal_wait_phases) and the computes of
- * plans (reductions of the program's dtype, or HICCL_BYTES exact copies) --
- * executed by ONE persistent kernel launch: each element runs after the
- * previous one has completed (a device-side ticket order with per-element
- * completion counters, no grid barrier), with the same stores, waits and
- * results as launching them one by one on a stream.
+ * start -> compute wait (comm.h:195-204); the stream-ordered port enqueues a
+ * hiccl_signal_wait_phases before every copy and reduction kernel.  A
+ * program is ONE launch of: the phases (run first, in order, by one wave,
+ * as hiccl_signal_wait_phases does), then the units of one batch of
+ * computes -- plans' computes, reductions of the program's dtype or
+ * HICCL_BYTES exact copies, all independent of each other -- which start
+ * only after the last phase.  Same stores, waits and results as the
+ * separate launches, one kernel boundary fewer per phase group.
  *
- * add_signal appends one phase (consecutive phases form one element, run
- *   in order by one wave); its epoch is supplied per launch.
+ * add_signal appends one phase (only before the first add_plan); its epoch
+ *   is supplied per launch.
  * add_plan appends the plan's computes as of this call (later adds to the
- *   plan are not seen): join != 0 puts them in the same element as the
- *   previous plan's (no ordering between them: independent outputs),
- *   otherwise they start after it.  The plan's dtype must be the program's
- *   or HICCL_BYTES; native accumulation only.
+ *   plan are not seen); the plan's dtype must be the program's or
+ *   HICCL_BYTES; native accumulation only.  Computes of several plans form
+ *   one batch: they must not depend on each other.
  * launch: epochs[p] for every phase p (+ *epoch_dev when not NULL, read at
  *   run time: graph replays), err / timeout_s as hiccl_signal_wait.  The
  *   first launch (and the first after a change) uploads the program's tables
- *   and cannot be captured into a graph.  One launch of a program at a time.
- * Limits: 48 elements, 64 phases per program.
+ *   and cannot be captured into a graph.  One launch of a program at a time
+ *   (launches on one stream).
+ * Limit: 64 phases per program.
  */
 typedef struct hiccl_program hiccl_program_t;
 int hiccl_program_create(hiccl_program_t **prog, int dtype, int device);
 int hiccl_program_add_signal(hiccl_program_t *prog, uint32_t *const *sig, int nsig, const uint32_t *const *wait,
                              int nwait);
-int hiccl_program_add_plan(hiccl_program_t *prog, const hiccl_reduce_plan_t *plan, int join);
-/* Cap the launch at max_wg workgroups (0: the default, 2 per CU).  Several
- * processes sharing one GPU (rehearsals) split it this way: a program's
- * workgroups wait on the GPU for earlier elements and peers' tokens. */
+int hiccl_program_add_plan(hiccl_program_t *prog, const hiccl_reduce_plan_t *plan);
+/* Cap the launch at max_wg workgroups (0: the default, 2-4 per CU).
+ * Processes sharing one GPU (rehearsals) split it this way: a program's
+ * workgroups wait on the GPU for its phases, i.e. for peers' tokens. */
 int hiccl_program_set_max_workgroups(hiccl_program_t *prog, int max_wg);
-int hiccl_program_num_segments(const hiccl_program_t *prog);
+int hiccl_program_num_units(const hiccl_program_t *prog);
 int hiccl_program_num_phases(const hiccl_program_t *prog);
 int hiccl_program_launch(hiccl_program_t *prog, const uint32_t *epochs, const uint32_t *epoch_dev, uint32_t *err,
                          double timeout_s, void *stream);

@@ -123,7 +123,7 @@ def test_program_argument_checks_on_host():
     assert lib.hiccl_program_create(None, L.HICCL_FLOAT32, 0) != 0
     assert lib.hiccl_program_create(ctypes.byref(h), 99, 0) != 0 and not h.value
     assert lib.hiccl_program_add_signal(None, None, 0, None, 0) != 0
-    assert lib.hiccl_program_add_plan(None, None, 0) != 0
+    assert lib.hiccl_program_add_plan(None, None) != 0
     assert lib.hiccl_program_launch(None, None, None, None, 1.0, None) != 0
-    assert lib.hiccl_program_num_segments(None) == 0 and lib.hiccl_program_num_phases(None) == 0
+    assert lib.hiccl_program_num_units(None) == 0 and lib.hiccl_program_num_phases(None) == 0
     lib.hiccl_program_destroy(None)

@@ -1,15 +1,15 @@
-"""GPU tier: step programs (include/hiccl_reduce.h hiccl_program_*).
+"""GPU tier: programs (include/hiccl_reduce.h hiccl_program_*).
 
-A program runs an ordered list -- signal/wait phases, exact byte copies
-(HICCL_BYTES plans), reductions (plans of the program's dtype) -- as ONE
-launch, each element after the previous one completed.  HiCCL::Comm records
-one per stream-ordered pipeline step (comm.h:195-204's transport -> compute
-order).  The checks: a reduction sees the bytes the copy before it wrote
-(small shapes with half tiles, large with full tiles), a chain of dependent
-elements, phases store / await their per-launch epochs (and epoch +
-*epoch_dev under graph replay), a wait that is never satisfied times out
-with the error word set while the grid still drains, relaunches reuse the
-device counters, and the reductions give the oracle's bits.
+A program is ONE launch of signal/wait phases followed by a batch of
+independent computes (exact byte copies from HICCL_BYTES plans, reductions
+of the program's dtype); HiCCL::Comm records its stream-ordered pipeline as
+a list of them.  The checks: no unit starts before the
+last phase is satisfied (a peer-like stream writes the source and then the
+flag while the program waits), consecutive programs see each other's
+results, phases store / await their per-launch epochs (and epoch +
+*epoch_dev under graph replay), relaunches reuse the gate word, a wait that
+is never satisfied times out with the error word set while the grid still
+drains, and the reductions give the oracle's bits.
 """
 import ctypes
 
@@ -44,71 +44,72 @@ def _inorder(xs):
 
 
 @pytest.mark.parametrize("count", [(1 << 18) + 3, (1 << 24) + 5], ids=["half_tiles", "full_tiles"])
-def test_copy_then_reduce_sees_the_copy(count):
-    """[copy src -> mid] then [out = mid + b]: the reduction reads what the
-    copy wrote in the same launch (bits of an in-order sum), over three
-    launches with new source contents each time."""
+def test_units_wait_for_the_phases(count):
+    """The program waits for a flag; another stream first rewrites the copy's
+    source, then sets the flag: the copy (and the reduction of the same
+    batch) must see the new source -- no unit ran before the gate opened.
+    Three launches with new contents each time; the program is capped at 64
+    workgroups so the other stream's kernels always find room on the GPU."""
     src = torch.empty(count, device=DEV)
     b = torch.empty(count, device=DEV)
-    mid = torch.full((count,), float("nan"), device=DEV)
-    out = torch.empty(count, device=DEV)
     hiccl_amd.fill_uniform(b, 7, 1)
-    cp = _copy_plan(mid, src, count * 4)
-    red = _sum_plan(out, [mid, b], count)
+    dst = torch.full((count,), float("nan"), device=DEV)
+    out = torch.empty(count, device=DEV)
+    flags = torch.zeros(4, dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    f = flags.data_ptr()
+    cp = _copy_plan(dst, src, count * 4)
+    red = _sum_plan(out, [src, b], count)
     prog = hiccl_amd.Program(torch.float32, device=0)
+    prog.add_signal([], [f])
     prog.add_plan(cp)
     prog.add_plan(red)
-    assert prog.segments() == 2
+    prog.set_max_workgroups(64)
+    assert prog.units() == 2 and prog.phases() == 1
+    other = torch.cuda.Stream()
+    tab = (ctypes.c_void_p * 1)(f)
     for it in range(3):
         hiccl_amd.fill_uniform(src, 100 + it, 0)
-        prog.launch()
         torch.cuda.synchronize()
-        exp = _inorder([src, b])
-        assert torch.equal(mid.view(torch.int32), src.view(torch.int32))
-        assert torch.equal(out.view(torch.int32), exp.view(torch.int32)), f"launch {it}"
+        prog.launch([it + 1], err=err.data_ptr(), timeout_s=20.0)
+        hiccl_amd.fill_uniform(src, 200 + it, 0, stream=other)  # the "peer": new data, then the token
+        L.check(L.lib().hiccl_signal_wait(tab, 1, None, 0, it + 1, None, 5.0, ctypes.c_void_p(other.cuda_stream)),
+                "signal_wait")
+        torch.cuda.synchronize()
+        assert err.item() == 0
+        assert torch.equal(dst.view(torch.int32), src.view(torch.int32)), f"launch {it}: a unit ran early"
+        assert torch.equal(out.view(torch.int32), _inorder([src, b]).view(torch.int32))
     prog.close()
 
 
-def test_dependent_chain_of_elements():
-    """out_k = out_{k-1} + x_k for 12 elements, alternating with byte copies
-    and self-signalling phases: every element must see its predecessor."""
+def test_chain_of_programs():
+    """out_k = out_{k-1} + x_k as 12 programs in a row (each with a phase):
+    every program sees the previous one's result (a kernel boundary)."""
     count = (1 << 20) + 7
     xs = [torch.empty(count, device=DEV) for _ in range(12)]
     for k, x in enumerate(xs):
         hiccl_amd.fill_uniform(x, 11, k)
     outs = [torch.empty(count, device=DEV) for _ in range(12)]
-    flags = torch.zeros(64, dtype=torch.int32, device=DEV)
-    prog = hiccl_amd.Program(torch.float32, device=0)
-    keep = []
-    prev = None
-    nph = 0
+    flags = torch.zeros(16, dtype=torch.int32, device=DEV)
+    progs, keep = [], []
     for k in range(12):
-        if prev is None:
-            c = _sum_plan(outs[k], [xs[k]], count)
-        else:
-            c = _sum_plan(outs[k], [prev, xs[k]], count)
+        c = _sum_plan(outs[k], [xs[k]] if k == 0 else [outs[k - 1], xs[k]], count)
         keep.append(c)
-        prog.add_plan(c)
-        if k % 3 == 1:  # a copy of the running sum, then a phase
-            cp_dst = torch.empty(count, device=DEV)
-            cp = _copy_plan(cp_dst, outs[k], count * 4)
-            keep += [cp, cp_dst]
-            prog.add_plan(cp)
-            f = flags.data_ptr() + 4 * nph
-            prog.add_signal([f], [f])
-            nph += 1
-            prev = cp_dst
-        else:
-            prev = outs[k]
-    epochs = list(range(40, 40 + nph))
-    prog.launch(epochs)
+        pr = hiccl_amd.Program(torch.float32, device=0)
+        f = flags.data_ptr() + 4 * k
+        pr.add_signal([f], [f])
+        pr.add_plan(c)
+        progs.append(pr)
+    for k, pr in enumerate(progs):
+        pr.launch([40 + k])
     torch.cuda.synchronize()
     acc = torch.zeros(count, device=DEV)
     for k in range(12):
         acc = acc + xs[k]
-        assert torch.equal(outs[k].view(torch.int32), acc.view(torch.int32)), f"element {k}"
-    assert flags[:nph].tolist() == epochs
-    prog.close()
+        assert torch.equal(outs[k].view(torch.int32), acc.view(torch.int32)), f"program {k}"
+    assert flags[:12].tolist() == [40 + k for k in range(12)]
+    for pr in progs:
+        pr.close()
 
 
 def test_phases_store_and_await_epochs_and_relaunch():
@@ -121,16 +122,25 @@ def test_phases_store_and_await_epochs_and_relaunch():
     fa, fb = flags.data_ptr(), flags.data_ptr() + 4
     prog = hiccl_amd.Program(torch.float32, device=0)
     prog.add_signal([fa], [fa])
+    prog.add_signal([fb], [fb])
     red = _sum_plan(out, [x, x], count)
     prog.add_plan(red)
-    prog.add_signal([fb], [fb])
-    assert prog.phases() == 2 and prog.segments() == 3
+    assert prog.phases() == 2 and prog.units() == 1
+    with pytest.raises(hiccl_amd.HicclError):
+        prog.add_signal([fa], [fa])  # phases precede the units
     for e in (5, 9, 13):
         prog.launch([e, e + 1], err=err.data_ptr(), timeout_s=5.0)
         torch.cuda.synchronize()
         assert flags[:2].tolist() == [e, e + 1]
         assert err.item() == 0
     assert torch.equal(out.view(torch.int32), (torch.zeros_like(x) + x + x).view(torch.int32))
+    # a phases-only program (the trailing tokens of a pipeline)
+    only = hiccl_amd.Program(torch.float32, device=0)
+    only.add_signal([fa], [])
+    only.launch([77])
+    torch.cuda.synchronize()
+    assert flags[0].item() == 77
+    only.close()
     prog.close()
 
 
@@ -145,7 +155,7 @@ def test_unsatisfied_wait_times_out_and_drains():
     err = torch.zeros(1, dtype=torch.int32, device=DEV)
     prog = hiccl_amd.Program(torch.float32, device=0)
     prog.add_signal([], [flags.data_ptr()])
-    red = _sum_plan(out, [x], count)
+    red = _sum_plan(out, [x], count)  # runs once the wait has given up
     prog.add_plan(red)
     prog.launch([1], err=err.data_ptr(), timeout_s=0.2)
     torch.cuda.synchronize()
@@ -215,7 +225,7 @@ def test_program_dtypes_match_oracle(oracle, dtype):
     prog.close()
 
 
-def test_joined_plans_and_refusals():
+def test_batch_of_plans_and_refusals():
     count = 1 << 18
     a = torch.empty(count, device=DEV)
     b = torch.empty(count, device=DEV)
@@ -226,8 +236,8 @@ def test_joined_plans_and_refusals():
     prog = hiccl_amd.Program(torch.float32, device=0)
     p1, p2 = _sum_plan(o1, [a, b], count), _sum_plan(o2, [b, a], count)
     prog.add_plan(p1)
-    prog.add_plan(p2, join=True)
-    assert prog.segments() == 1
+    prog.add_plan(p2)
+    assert prog.units() == 2
     prog.launch()
     torch.cuda.synchronize()
     assert torch.equal(o1.view(torch.int32), _inorder([a, b]).view(torch.int32))
