@@ -14,7 +14,11 @@
 //   3. every rank hipFrees A and hipMallocs B of the same sizes (the
 //      allocator usually hands A's addresses back), writes nonces, exports
 //   4. every rank opens every peer's B and reads its nonces through the new
-//      mappings, then closes them
+//      mappings, then closes them -- except in "late": there the A mappings
+//      were kept open through 3-4 and are closed only now, while B's are
+//      still open, and B is read once more after that close (the order a
+//      capped retirement produces: an old mapping of a base closed after a
+//      newer one of the same base was opened)
 // Small buffers (1 MiB) are sub-allocated by HIP, large ones (64 MiB) are
 // allocations of their own.  The reference exchanges hipIpcMemHandle_t
 // across processes the same way (/root/reference/misc/test.md:85).
@@ -103,10 +107,11 @@ int main(int argc, char **argv) {
   const int nbufs[2] = {1, 3};
   for (size_t bytes : sizes)
     for (int nbuf : nbufs)
-      for (const char *variant : {"close", "keep", "mixed"}) {
+      for (const char *variant : {"close", "keep", "mixed", "late"}) {
         const std::string v = variant;
         const bool do_close = v == "close" || (v == "mixed" && me % 2 == 0);
-        long st[5] = {0, 0, 0, 0, 0};  // reads, first ok, recycled, copy ok, kernel ok
+        const bool late = v == "late";
+        long st[7] = {0, 0, 0, 0, 0, 0, 0};  // reads, first ok, recycled, copy ok, kernel ok, late reads, late ok
         std::vector<void *> kept;
         for (int r = 0; r < rounds; r++) {
           std::vector<Export> ea, eb;
@@ -122,11 +127,13 @@ int main(int argc, char **argv) {
             }
           for (void *m : ma) {
             if (do_close) check(hipIpcCloseMemHandle(m), "close A");
-            else kept.push_back(m);
+            else if (!late) kept.push_back(m);
           }
           MPI_Barrier(MPI_COMM_WORLD);
           for (void *p : a) check(hipFree(p), "free A");  // 3.
           std::vector<void *> b = alloc_and_export(bytes, nbuf, me, np, eb);
+          std::vector<void *> mb;
+          std::vector<uint64_t> nb;
           for (int p = 0; p < np; p++)  // 4.
             for (int j = 0; j < nbuf && p != me; j++) {
               const Export &f = eb[(size_t)p * nbuf + j];
@@ -138,20 +145,30 @@ int main(int argc, char **argv) {
               st[0]++;
               st[3] += got & 1;
               st[4] += (got >> 1) & 1;
-              check(hipIpcCloseMemHandle(m), "close B");
+              mb.push_back(m);
+              nb.push_back(f.nonce);
             }
+          if (late) {  // close A's mappings now, then read B through its (still open) mappings again
+            for (void *m : ma) check(hipIpcCloseMemHandle(m), "late close A");
+            for (size_t i = 0; i < mb.size(); i++) {
+              st[5]++;
+              st[6] += read_views(mb[i], nb[i], scratch) == 3;
+            }
+          }
+          for (void *m : mb) check(hipIpcCloseMemHandle(m), "close B");
           MPI_Barrier(MPI_COMM_WORLD);
           for (void *p : b) check(hipFree(p), "free B");
           MPI_Barrier(MPI_COMM_WORLD);
         }
         for (void *m : kept) check(hipIpcCloseMemHandle(m), "close kept");
-        long tot[5];
-        MPI_Reduce(st, tot, 5, MPI_LONG, MPI_SUM, 0, MPI_COMM_WORLD);
+        long tot[7];
+        MPI_Reduce(st, tot, 7, MPI_LONG, MPI_SUM, 0, MPI_COMM_WORLD);
         if (me == 0)
           std::printf("{\"variant\": \"%s\", \"ranks\": %d, \"bytes\": %zu, \"buffers\": %d, \"rounds\": %d, "
                       "\"devices\": %d, \"reads\": %ld, \"first_mapping_ok\": %ld, \"recycled_address\": %ld, "
-                      "\"second_mapping_copy_engine_ok\": %ld, \"second_mapping_kernel_ok\": %ld}\n",
-                      variant, np, bytes, nbuf, rounds, ndev, tot[0], tot[1], tot[2], tot[3], tot[4]);
+                      "\"second_mapping_copy_engine_ok\": %ld, \"second_mapping_kernel_ok\": %ld, "
+                      "\"late_close_reads\": %ld, \"after_late_close_ok\": %ld}\n",
+                      variant, np, bytes, nbuf, rounds, ndev, tot[0], tot[1], tot[2], tot[3], tot[4], tot[5], tot[6]);
         std::fflush(stdout);
         MPI_Barrier(MPI_COMM_WORLD);
       }

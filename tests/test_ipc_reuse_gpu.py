@@ -3,7 +3,9 @@
 tests/cpp/ipc_reuse.cpp (2 or 4 MPI processes, all-to-all like a
 communicator) runs, per round: every rank exports fresh allocations A, every
 peer opens them and then closes its mappings ("close"), keeps them
-("keep") or -- "mixed" -- odd ranks keep and even ranks close; every rank
+("keep"), -- "mixed" -- odd ranks keep and even ranks close, or -- "late" --
+keeps them until it has opened the next allocation at the same address and
+closes them then (what a capped retirement does); every rank
 frees A, allocates B of the same sizes (usually at A's addresses) and
 exports them; the peers open B and read the owner's nonces through the copy
 engine and through a kernel.  Cases: 64 MiB (own allocations) and 1 MiB
@@ -37,7 +39,7 @@ def test_ipc_close_then_reopen_recycled_address_outcome(ranks):
                        capture_output=True, text=True, env=env, cwd="/tmp")
     assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
     rows = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(rows) == 12, p.stdout
+    assert len(rows) == 16, p.stdout
     out = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, "ipc_reuse.jsonl"), "a") as f:
