@@ -111,7 +111,8 @@ int main(int argc, char **argv) {
         const std::string v = variant;
         const bool do_close = v == "close" || (v == "mixed" && me % 2 == 0);
         const bool late = v == "late";
-        long st[7] = {0, 0, 0, 0, 0, 0, 0};  // reads, first ok, recycled, copy ok, kernel ok, late reads, late ok
+        // B reads, A ok, recycled, B copy ok, B kernel ok, late reads, late ok, A opens, A open failed, B open failed
+        long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         std::vector<void *> kept;
         for (int r = 0; r < rounds; r++) {
           std::vector<Export> ea, eb;
@@ -121,7 +122,12 @@ int main(int argc, char **argv) {
             for (int j = 0; j < nbuf && p != me; j++) {
               const Export &e = ea[(size_t)p * nbuf + j];
               void *m = nullptr;
-              check(hipIpcOpenMemHandle(&m, e.h, hipIpcMemLazyEnablePeerAccess), "open A");
+              st[7]++;
+              if (hipIpcOpenMemHandle(&m, e.h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                (void)hipGetLastError();  // recorded, not fatal: the outcome is what this program measures
+                st[8]++;
+                continue;
+              }
               if (read_views(m, e.nonce, scratch) == 3) st[1]++;
               ma.push_back(m);
             }
@@ -140,9 +146,13 @@ int main(int argc, char **argv) {
               for (int i = 0; i < nbuf; i++)
                 if (f.addr == ea[(size_t)p * nbuf + i].addr) st[2]++;
               void *m = nullptr;
-              check(hipIpcOpenMemHandle(&m, f.h, hipIpcMemLazyEnablePeerAccess), "open B");
-              const int got = read_views(m, f.nonce, scratch);
               st[0]++;
+              if (hipIpcOpenMemHandle(&m, f.h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                (void)hipGetLastError();
+                st[9]++;
+                continue;
+              }
+              const int got = read_views(m, f.nonce, scratch);
               st[3] += got & 1;
               st[4] += (got >> 1) & 1;
               mb.push_back(m);
@@ -161,14 +171,16 @@ int main(int argc, char **argv) {
           MPI_Barrier(MPI_COMM_WORLD);
         }
         for (void *m : kept) check(hipIpcCloseMemHandle(m), "close kept");
-        long tot[7];
-        MPI_Reduce(st, tot, 7, MPI_LONG, MPI_SUM, 0, MPI_COMM_WORLD);
+        long tot[10];
+        MPI_Reduce(st, tot, 10, MPI_LONG, MPI_SUM, 0, MPI_COMM_WORLD);
         if (me == 0)
           std::printf("{\"variant\": \"%s\", \"ranks\": %d, \"bytes\": %zu, \"buffers\": %d, \"rounds\": %d, "
-                      "\"devices\": %d, \"reads\": %ld, \"first_mapping_ok\": %ld, \"recycled_address\": %ld, "
+                      "\"devices\": %d, \"first_opens\": %ld, \"first_open_failed\": %ld, \"first_mapping_ok\": %ld, "
+                      "\"reads\": %ld, \"second_open_failed\": %ld, \"recycled_address\": %ld, "
                       "\"second_mapping_copy_engine_ok\": %ld, \"second_mapping_kernel_ok\": %ld, "
                       "\"late_close_reads\": %ld, \"after_late_close_ok\": %ld}\n",
-                      variant, np, bytes, nbuf, rounds, ndev, tot[0], tot[1], tot[2], tot[3], tot[4], tot[5], tot[6]);
+                      variant, np, bytes, nbuf, rounds, ndev, tot[7], tot[8], tot[1], tot[0], tot[9], tot[2], tot[3],
+                      tot[4], tot[5], tot[6]);
         std::fflush(stdout);
         MPI_Barrier(MPI_COMM_WORLD);
       }
