@@ -496,12 +496,20 @@ class Comm {
       // the GPU (single-GPU rehearsals only) split its workgroup slots so
       // every rank's kernels stay resident while the others wait for them
       rec.max_wg = device_ranks > 1 ? program_grid_share() : 0;
+      // A step's transports in the reference's order (comm.h:188-204: every
+      // transport starts, then each is waited for): all ready phases, all
+      // copies as ONE batch, all done phases, then the computes as one batch
+      // -- two launches per step (the fused transfers' tail phases ride in
+      // the next step's first program).
+      rec.join_all_copies = true;
       CommBench::step_recorder() = &rec;
       const size_t nl = command_batch.size();
       std::vector<typename std::list<Command<T>>::iterator> it(nl);
       for (size_t i = 0; i < nl; i++) it[i] = command_batch[i].begin();
       while (it[0] != command_batch[0].end()) {
-        for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue(s);
+        for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue_pre(s);
+        for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue_copies(s);
+        for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue_post(s);
         for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
         for (size_t i = 0; i < nl; i++) {
           it[i]->comm->enqueue_tail(s);

@@ -749,6 +749,7 @@ struct StepRecorder {
   bool cur_units = false;
   int last = 0;                      // kind of the last batch appended: 1 copies, 2 computes
   const void *last_owner = nullptr;  // the transport whose copies were appended last
+  bool join_all_copies = false;      // one batch for the copies of every transport of a step
 
   void open() {
     if (cur) return;
@@ -1006,6 +1007,17 @@ class Comm {
   void enqueue_tail(hipStream_t s) {
     signal_wait(tail_sig, tail_wait, sig_epoch(), graph_epoch, flags->err, s, epoch_fn());
   }
+  // enqueue() in three parts, so that a step's transports can be issued the
+  // way the reference starts them -- all together (comm.h:188-191) -- every
+  // ready phase first, then every copy, then every done phase (programs).
+  void enqueue_pre(hipStream_t s) {
+    ++epoch;
+    signal_wait(pre_sig, pre_wait, sig_epoch(), graph_epoch, flags->err, s, epoch_fn());
+  }
+  void enqueue_copies(hipStream_t s) { launch_copies(s); }
+  void enqueue_post(hipStream_t s) {
+    signal_wait(post_sig, post_wait, sig_epoch(), graph_epoch, flags->err, s, epoch_fn());
+  }
   // A recorded step program runs instead of enqueue(): the execution still
   // counts (the program's phases read sig_epoch() at each launch).
   void advance() { ++epoch; }
@@ -1236,7 +1248,7 @@ class Comm {
   // plan's completion event: enqueue without one
   void launch_plan(hiccl_reduce_plan_t *p, hipStream_t s, const char *what) {
     flush_signals();  // queued signal/wait steps precede this kernel on the stream
-    if (step_recorder()) return record_plan(p, 1, this);
+    if (StepRecorder *r = step_recorder()) return record_plan(p, 1, r->join_all_copies ? nullptr : this);
     if (hiccl_reduce_plan_enqueue(p, s)) die(what, hiccl_last_error());
   }
 
