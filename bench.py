@@ -162,7 +162,9 @@ def run_c5(world, args, allow_shared=False):
     out = {"workload": f"C5: all-reduce of {count * world * 4 >> 20} MiB fp32 per rank, {world} ranks, hierarchy "
                        f"{{{hier}}} {{{libs}}}, pipedepth 128 (collectives/main.cpp:151-155)",
            "env_scrubbed": scrubbed, "devices_counted_unmasked": ndev}
-    fused = {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "1"}
+    # step programs asked for explicitly (the default with one GPU per rank),
+    # so _noprog below stays an A/B whatever the library's default
+    fused = {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "1", "HICCL_STEP_PROGRAM": "1"}
     modes = [("host", {"HICCL_STREAM_ORDERED": "0"}, hier, libs),
              ("stream_graph", {"HICCL_STREAM_ORDERED": "1", "HICCL_GRAPH": "1", "HICCL_FUSED_GATHER": "0"}, hier, libs),
              ("stream_graph_fused", fused, hier, libs),

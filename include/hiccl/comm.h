@@ -470,7 +470,8 @@ class Comm {
     CommBench::flush_signals();  // (the last step's done tokens)
   }
 
-  // Programs (HICCL_STEP_PROGRAM, on by default in stream-ordered mode): the
+  // Programs (HICCL_STEP_PROGRAM; stream-ordered mode, on by default with one
+  // GPU per rank, want_programs()): the
   // first stream-ordered run() records the enqueue sequence above -- per
   // step every library's ready tokens, copies and done tokens, the computes
   // in reverse library order, the fused transfers' done tokens -- as a list
@@ -543,9 +544,16 @@ class Comm {
     return std::max(8, cus / device_ranks);
   }
 
+  // Default: programs when every rank drives its own GPU.  Ranks sharing one
+  // GPU (forced single-GPU rehearsals) launch per element unless
+  // HICCL_STEP_PROGRAM=1: a program's workgroups wait on the device for the
+  // peer's token while the peer's kernels need that device to produce it
+  // (2 ranks, pipedepth 128, 64 MiB/rank: graph + fused 2.67-2.93 ms with
+  // programs vs 1.57-1.58 without, profiles/r03i_c5_prog_ab.jsonl; one
+  // process per GPU: 15.2 vs 22.1 us per step, profiles/r03g_progstep.jsonl).
   bool want_programs() {
     const char *env = std::getenv("HICCL_STEP_PROGRAM");
-    int on = !(env && std::string(env) == "0");
+    int on = env ? std::string(env) != "0" : device_ranks <= 1;
     for (auto &lst : command_batch)
       for (auto &c : lst) on = on && c.comm->recordable();
     MPI_Allreduce(MPI_IN_PLACE, &on, 1, MPI_INT, MPI_LAND, CommBench::comm_mpi);

@@ -32,13 +32,23 @@ def mpirun(np_, exe, args, timeout=180, streamed=True, fused=False, engine="auto
            stream_env=None, queues=True, extra_env=None):
     """streamed: HICCL_STREAM_ORDERED=force -- every rank here shares the box's
     one GPU, where the library would otherwise fall back to host-driven mode
-    (tested by test_shared_device_falls_back_to_host_driven)."""
+    (tested by test_shared_device_falls_back_to_host_driven).  Stream-ordered
+    runs ask for step programs (HICCL_STEP_PROGRAM=1), the default with one
+    GPU per rank, which ranks sharing a GPU would otherwise not use
+    (test_shared_device_defaults_to_per_element_launches); extra_env wins."""
     assert np_ <= 8
     if stream_env is None:
         stream_env = "force" if streamed else "0"
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED=stream_env,
                HICCL_FUSED_GATHER="1" if fused else "0", HICCL_SIGNAL_TIMEOUT="10", HICCL_ENGINE=engine,
-               HICCL_GRAPH="1" if graph else "0", HICCL_DRIVER_REPEAT=str(repeat), **(extra_env or {}))
+               HICCL_GRAPH="1" if graph else "0", HICCL_DRIVER_REPEAT=str(repeat))
+    if streamed:
+        env["HICCL_STEP_PROGRAM"] = "1"
+    for k, v in (extra_env or {}).items():  # None: unset
+        if v is None:
+            env.pop(k, None)
+        else:
+            env[k] = v
     if np_ > 4 and queues:
         # every rank on the box's one GPU: 8 processes x 4 hardware queues
         # oversubscribe the device's queue slots, and a spinning stream-ordered
@@ -143,6 +153,19 @@ def test_allreduce_bits_step_program_ab(tmp_path, oracle, np_, count, depth, hie
         got = np.fromfile(f"{prefix}.rank{r}.bin", dtype=np.float32)
         exp = mem[(r, ("recv",))]
         assert got.tobytes() == exp.tobytes(), f"rank {r}: {int((got != exp).sum())} differ"
+
+
+@pytest.mark.parametrize("graph", [False, True], ids=["stream", "stream-graph"])
+def test_shared_device_defaults_to_per_element_launches(graph):
+    """Ranks sharing the GPU, stream-ordered forced, HICCL_STEP_PROGRAM unset:
+    one launch per element of a step (a program's waiting workgroups would
+    hold the device the peer needs, profiles/r03i_c5_prog_ab.jsonl); the KAT
+    passes."""
+    rc, out = mpirun(2, HIP, [8, 4099, 1, 1, 3, 0, 0, "2", "ipc"], graph=graph,
+                     extra_env={"HICCL_STEP_PROGRAM": None})
+    assert rc == 0, out[-3000:]
+    assert "PASSED!" in out and "stream-ordered" in out
+    assert "step programs" not in out, out[-2000:]
 
 
 @pytest.mark.parametrize("np_,hier,libs", [(2, "2", "ipc"), (4, "2,2", "mpi,ipc"), (4, "4", "ipc_get"),
