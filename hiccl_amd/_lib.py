@@ -32,6 +32,9 @@ HICCL_ENGINE_AUTO = 0
 HICCL_ENGINE_TILE = 1
 HICCL_ENGINE_PHASE = 2
 
+HICCL_PEER_STORES = 1
+HICCL_PEER_LOADS = 2
+
 HICCL_SCHED_AUTO = 0
 HICCL_SCHED_STATIC = 1
 HICCL_SCHED_DYNAMIC = 2
@@ -80,6 +83,8 @@ _SIGS = {
     "hiccl_reduce_plan_set_engine": (ctypes.c_int, [_vp, ctypes.c_int]),
     "hiccl_reduce_plan_set_config": (ctypes.c_int, [_vp, ctypes.POINTER(ReduceConfig)]),
     "hiccl_reduce_plan_engine": (ctypes.c_int, [_vp]),
+    "hiccl_reduce_plan_set_peer": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "hiccl_reduce_plan_peer": (ctypes.c_int, [_vp]),
     "hiccl_reduce_plan_add": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_size_t]),
     "hiccl_reduce_plan_launch": (ctypes.c_int, [_vp, _vp]),
     "hiccl_reduce_plan_enqueue": (ctypes.c_int, [_vp, _vp]),

@@ -139,6 +139,16 @@ class Compute:
         cfg = L.ReduceConfig(**config)
         L.check(L.lib().hiccl_reduce_plan_set_config(self._plan, ctypes.byref(cfg)), "plan_set_config")
 
+    def set_peer(self, flags):
+        """Peer-memory policy of the plan's launches (hiccl_reduce_plan_set_peer):
+        HICCL_PEER_STORES (outputs in another GPU's memory: system-scope
+        write-through stores) | HICCL_PEER_LOADS (inputs there: system-scope
+        loads).  Same results."""
+        L.check(L.lib().hiccl_reduce_plan_set_peer(self._plan, flags), "plan_set_peer")
+
+    def peer(self):
+        return L.lib().hiccl_reduce_plan_peer(self._plan)
+
     def engine(self):
         """Engine the last upload resolved to (HICCL_ENGINE_TILE / _PHASE)."""
         return L.lib().hiccl_reduce_plan_engine(self._plan)

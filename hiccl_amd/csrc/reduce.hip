@@ -89,18 +89,28 @@ __device__ __forceinline__ rsrc_t make_rsrc(const char *base, uint32_t nbytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nbytes, kRsrcFlags);
 }
 
-// Cache policy, POL = 10*store + load.  load: 0 default, 1 nt (aux bit 1).
+// Cache policy, POL = 10*store + load.  load: 0 default, 1 nt (aux bit 1),
+// 2 system scope (sc0 sc1: coherent with a peer GPU's writes -- the
+// reading XCD's L2 does not serve a line of peer memory it cached earlier).
 // store: 0 default, 1 nt, 2 sc1 (aux bit 4: write-through, line dropped
-// from the XCD L2).
+// from the XCD L2), 3 system scope (sc0 sc1: written through to the memory
+// that owns the line, a peer GPU's HBM over xGMI included -- nt stores are
+// not write-through and may sit dirty in this XCD's L2 after the kernel).
+// The system-scope forms are the PEER policies of plans whose outputs or
+// inputs live in another GPU's memory (hiccl_reduce_plan_set_peer).
+constexpr int kPolLoadSys = 2;
+constexpr int kPolStoreSys = 3;
+
 template <int POL>
 __device__ __forceinline__ u32x4 load_pkt(rsrc_t r, uint32_t voff) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, (POL % 10) == 1 ? 2 : 0);
+  constexpr int lp = POL % 10;
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, lp == 1 ? 2 : lp == kPolLoadSys ? 17 : 0);
 }
 
 template <int POL>
 __device__ __forceinline__ void store_pkt(rsrc_t r, uint32_t voff, u32x4 v) {
   constexpr int sp = POL / 10;
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, 0, sp == 1 ? 2 : sp == 2 ? 16 : 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, 0, sp == 1 ? 2 : sp == 2 ? 16 : sp == kPolStoreSys ? 17 : 0);
 }
 
 // bf16 <-> f32.  f32 -> bf16 is round-to-nearest-even; on gfx950 the cast
@@ -317,16 +327,23 @@ struct ArgInputs {
   __device__ const char *operator()(int k) const { return p[k]; }
 };
 
-template <class Op, class Inputs>
+// Under the peer policies the plain scalar accesses are bracketed by
+// system-scope fences instead (an acquire before the loads: this XCD's L2
+// drops lines of peer memory; a release after the stores: its dirty lines
+// are written back) -- only the workgroup owning a compute's first unit,
+// and only when the compute has a head or a tail.
+template <class Op, int POL = 11, class Inputs>
 __device__ __forceinline__ void scalar_part(char *out, Inputs in, uint32_t n, uint32_t head,
                                             uint64_t npkt, uint32_t tail, int tid) {
   constexpr int V = kPacket / Op::kEsz;
   if (tid >= (int)(head + tail)) return;
+  if constexpr (POL % 10 == kPolLoadSys) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   uint64_t e = (tid < (int)head) ? (uint64_t)tid : (uint64_t)head + npkt * V + (tid - head);
   uint64_t off = e * Op::kEsz;
   typename Op::sacc_t acc = Op::szero();
   for (uint32_t k = 0; k < n; k++) acc = Op::sadd(acc, in(k) + off);
   Op::sstore(out + off, acc);
+  if constexpr (POL / 10 == kPolStoreSys) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 // One group of G inputs (G static): G descriptor builds (scalar), then G*U
@@ -610,7 +627,7 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_plan(PlanArgs a) {
     const PlanDesc d = load_desc(a.desc, c);
     const uint64_t lt = t - d.tile_begin;
     TableInputs raw{a.ptrs + (uint64_t)c * a.stride};
-    if (lt == 0) scalar_part<Op>(d.out, raw, d.n, d.head, d.npkt, d.tail, tid);
+    if (lt == 0) scalar_part<Op, POL>(d.out, raw, d.n, d.head, d.npkt, d.tail, tid);
     const uint64_t pkt0 = lt * TILE;
     if (pkt0 >= d.npkt) {  // a scalar-only compute: nothing to load or store
       hook();
@@ -776,7 +793,7 @@ struct ProgPhase {
 };
 
 struct ProgArgs {
-  const PlanDesc *desc;  // computes of the unit batch; pad bit 0: exact byte copy
+  const PlanDesc *desc;  // computes of the unit batch; pad bit 0: exact byte copy, bits 1-2: peer flags
   const char *const *ptrs;
   const uint32_t *unit_comp;
   const ProgPhase *phase;
@@ -837,18 +854,32 @@ __device__ __forceinline__ void prog_gate_wait(const ProgArgs &a, uint32_t seq) 
   }
 }
 
-template <class Op, int U>
+template <class Op, int U, int POL>
 __device__ __forceinline__ void prog_unit_of(const PlanDesc &d, TableInputs raw, uint64_t lt, int tid,
                                              const uint32_t (&voff)[U]) {
   constexpr uint64_t TILE = (uint64_t)kProgBlock * U;
-  if (lt == 0) scalar_part<Op>(d.out, raw, d.n, d.head, d.npkt, d.tail, tid);
+  if (lt == 0) scalar_part<Op, POL>(d.out, raw, d.n, d.head, d.npkt, d.tail, tid);
   const uint64_t pkt0 = lt * TILE;
   if (pkt0 >= d.npkt) return;
   const uint64_t shift = (uint64_t)d.head * Op::kEsz;
   Shifted<TableInputs> in{raw, shift};
   const uint64_t left = d.npkt - pkt0;
   const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
-  tile_body<Op, U, kProgPol>(d.out + shift, in, d.n, pkt0 * kPacket, tile_bytes, voff);
+  tile_body<Op, U, POL>(d.out + shift, in, d.n, pkt0 * kPacket, tile_bytes, voff);
+}
+
+// A unit under its compute's peer policy (the plan's hiccl_reduce_plan_set_peer
+// flags, kept in the descriptor: bit 0 stores, bit 1 loads; workgroup-uniform).
+template <class Op, int U>
+__device__ __forceinline__ void prog_unit_peer(uint32_t peer, const PlanDesc &d, TableInputs raw, uint64_t lt,
+                                               int tid, const uint32_t (&voff)[U]) {
+  constexpr int L = kProgPol % 10, S = kProgPol / 10;
+  switch (peer & 3u) {
+    case 0: prog_unit_of<Op, U, kProgPol>(d, raw, lt, tid, voff); break;
+    case 1: prog_unit_of<Op, U, 10 * kPolStoreSys + L>(d, raw, lt, tid, voff); break;
+    case 2: prog_unit_of<Op, U, 10 * S + kPolLoadSys>(d, raw, lt, tid, voff); break;
+    default: prog_unit_of<Op, U, 10 * kPolStoreSys + kPolLoadSys>(d, raw, lt, tid, voff); break;
+  }
 }
 
 template <class Op, int U>
@@ -874,12 +905,12 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
     const uint32_t c = a.unit_comp ? ((ConstU32 *)a.unit_comp)[t] : 0u;
     const ConstDesc *q = (const ConstDesc *)a.desc + c;
     const PlanDesc d = load_desc(a.desc, c);
-    const bool bytes = (q->pad & 1u) != 0;
+    const uint32_t flags = q->pad;  // bit 0: exact byte copy; bits 1-2: peer stores / peer loads
     TableInputs raw{a.ptrs + (uint64_t)c * a.stride};
-    if (bytes)
-      prog_unit_of<OpRaw, U>(d, raw, t - d.tile_begin, tid, voff);
+    if (flags & 1u)
+      prog_unit_peer<OpRaw, U>(flags >> 1, d, raw, t - d.tile_begin, tid, voff);
     else
-      prog_unit_of<Op, U>(d, raw, t - d.tile_begin, tid, voff);
+      prog_unit_peer<Op, U>(flags >> 1, d, raw, t - d.tile_begin, tid, voff);
   }
 }
 
@@ -1305,37 +1336,60 @@ uint64_t unit_pkts(int engine, int dtype, int acc, int unroll) {
 
 typedef void (*plan_fn)(const PlanArgs &, dim3, hipStream_t);
 
-template <class Op, int ENG, int U>
+template <class Op, int ENG, int U, int POL = kDefPol>
 void launch_plan_t(const PlanArgs &a, dim3 grid, hipStream_t s) {
   constexpr int B = ENG == kPhase ? kPhBlock : kPlanBlock;
-  hipLaunchKernelGGL((k_reduce_plan<Op, B, U, kDefPol, ENG>), grid, dim3(B), 0, s, a);
+  hipLaunchKernelGGL((k_reduce_plan<Op, B, U, POL, ENG>), grid, dim3(B), 0, s, a);
 }
 
-template <class Op, bool TUNED>
-plan_fn pick_plan_eng(int engine, int unroll) {
-  if (engine == HICCL_ENGINE_PHASE) return launch_plan_t<Op, kPhase, phase_p<Op>()>;
+// The plan kernels' cache policy: nt loads and stores, or a plan's peer
+// policy (hiccl_reduce_plan_set_peer: system-scope stores and/or loads) --
+// those in the PHASE engine's default shape and TILE at U = 4 (and 2 for the
+// headline types: a pipeline step's small batches).
+int plan_pol(int peer) {
+  return 10 * ((peer & HICCL_PEER_STORES) ? kPolStoreSys : kDefPol / 10) +
+         ((peer & HICCL_PEER_LOADS) ? kPolLoadSys : kDefPol % 10);
+}
+
+template <class Op, bool TUNED, int POL>
+plan_fn pick_plan_pol(int engine, int unroll) {
+  constexpr bool DEF = POL == kDefPol;
+  if (engine == HICCL_ENGINE_PHASE) return launch_plan_t<Op, kPhase, phase_p<Op>(), POL>;
   switch (unroll) {
     case 0:
-    case 4: return launch_plan_t<Op, kTile, 4>;
-    case 2: if constexpr (TUNED) return launch_plan_t<Op, kTile, 2>; break;
-    case 8: if constexpr (TUNED) return launch_plan_t<Op, kTile, 8>; break;
-    case 16: if constexpr (TUNED) return launch_plan_t<Op, kTile, 16>; break;
-    case 1: if constexpr (TUNED) return launch_plan_t<Op, kTile, 1>; break;
+    case 4: return launch_plan_t<Op, kTile, 4, POL>;
+    case 2: if constexpr (TUNED) return launch_plan_t<Op, kTile, 2, POL>; break;
+    case 8: if constexpr (TUNED && DEF) return launch_plan_t<Op, kTile, 8>; break;
+    case 16: if constexpr (TUNED && DEF) return launch_plan_t<Op, kTile, 16>; break;
+    case 1: if constexpr (TUNED && DEF) return launch_plan_t<Op, kTile, 1>; break;
     default: break;
   }
   return nullptr;
 }
 
-plan_fn pick_plan(int dtype, int acc, int engine, int unroll) {
+template <class Op, bool TUNED>
+plan_fn pick_plan_eng(int engine, int unroll, int pol) {
+  constexpr int L = kDefPol % 10, S = kDefPol / 10;
+  switch (pol) {
+    case kDefPol: return pick_plan_pol<Op, TUNED, kDefPol>(engine, unroll);
+    case 10 * kPolStoreSys + L: return pick_plan_pol<Op, TUNED, 10 * kPolStoreSys + L>(engine, unroll);
+    case 10 * S + kPolLoadSys: return pick_plan_pol<Op, TUNED, 10 * S + kPolLoadSys>(engine, unroll);
+    case 10 * kPolStoreSys + kPolLoadSys:
+      return pick_plan_pol<Op, TUNED, 10 * kPolStoreSys + kPolLoadSys>(engine, unroll);
+    default: return nullptr;
+  }
+}
+
+plan_fn pick_plan(int dtype, int acc, int engine, int unroll, int pol = kDefPol) {
   switch (dtype) {
-    case HICCL_FLOAT32: return pick_plan_eng<OpF32, true>(engine, unroll);
+    case HICCL_FLOAT32: return pick_plan_eng<OpF32, true>(engine, unroll, pol);
     case HICCL_BFLOAT16:
-      return acc == HICCL_ACC_WIDE ? pick_plan_eng<OpBF16Wide, false>(engine, unroll)
-                                   : pick_plan_eng<OpBF16, true>(engine, unroll);
-    case HICCL_FLOAT64: return pick_plan_eng<OpF64, false>(engine, unroll);
-    case HICCL_UINT64: return pick_plan_eng<OpU64, false>(engine, unroll);
-    case HICCL_INT32: return pick_plan_eng<OpI32, false>(engine, unroll);
-    case HICCL_BYTES: return pick_plan_eng<OpRaw, false>(engine, unroll);
+      return acc == HICCL_ACC_WIDE ? pick_plan_eng<OpBF16Wide, false>(engine, unroll, pol)
+                                   : pick_plan_eng<OpBF16, true>(engine, unroll, pol);
+    case HICCL_FLOAT64: return pick_plan_eng<OpF64, false>(engine, unroll, pol);
+    case HICCL_UINT64: return pick_plan_eng<OpU64, false>(engine, unroll, pol);
+    case HICCL_INT32: return pick_plan_eng<OpI32, false>(engine, unroll, pol);
+    case HICCL_BYTES: return pick_plan_eng<OpRaw, false>(engine, unroll, pol);
     default: return nullptr;
   }
 }
@@ -1469,6 +1523,7 @@ struct hiccl_reduce_plan {
   int unroll = kDefUnroll;         // TILE packets per lane, resolved at upload
   double mean_n = 0;               // packet-weighted inputs per compute
   int bpc = 1;                     // workgroups per CU, resolved at upload
+  int peer = 0;                    // hiccl_reduce_plan_set_peer flags
   size_t esz = 0;
   struct Comp {
     void *out;
@@ -1505,7 +1560,10 @@ namespace {
 // packets of packet-weighted mean `mean_n` inputs.
 Cfg plan_cfg(const hiccl_reduce_plan *p, uint64_t npkt, double mean_n) {
   Cfg c = resolve(&p->req);
+  const bool auto_unroll = !c.unroll;
   finish_cfg(c, npkt, mean_n, p->dtype, p->device);  // (kPlanBlock == kDefBlock)
+  // peer policies exist at TILE U = 4 / 2 only: wide tiles become U = 4
+  if (p->peer && c.engine == HICCL_ENGINE_TILE && auto_unroll && c.unroll != 2) c.unroll = kDefUnroll;
   return c;
 }
 
@@ -1593,9 +1651,12 @@ int plan_upload(hiccl_reduce_plan *p, hipStream_t s) {
 
 // One plan-kernel launch of `a` (desc, ptrs, unit_comp, units, stride set),
 // shaped by `c` (engine and shape resolved).
-int launch_plan(PlanArgs a, int dtype, const Cfg &c, double mean_n, int dev, hipStream_t s) {
-  plan_fn fn = pick_plan(dtype, c.acc, c.engine, c.unroll);
-  if (!fn) return fail(hipErrorInvalidValue, "plan: unsupported dtype / shape");
+int launch_plan(PlanArgs a, int dtype, const Cfg &c, double mean_n, int dev, hipStream_t s, int pol = kDefPol) {
+  plan_fn fn = pick_plan(dtype, c.acc, c.engine, c.unroll, pol);
+  if (!fn)
+    return fail(hipErrorInvalidValue, pol == kDefPol ? "plan: unsupported dtype / shape"
+                                                     : "plan: no peer-policy kernel for this shape (PHASE default, "
+                                                       "TILE unroll 4, f32 / bf16 also 2)");
   const uint64_t units = a.t_end - a.t_begin;
   uint64_t grid = c.grid > 0 ? (uint64_t)c.grid : (uint64_t)device_cus(dev) * c.bpc;
   if (grid > units) grid = units;
@@ -1611,7 +1672,7 @@ int plan_kernel(hiccl_reduce_plan *p, hipStream_t s) {
   c.unroll = p->unroll;
   c.block = p->engine == HICCL_ENGINE_PHASE ? kPhBlock : kPlanBlock;
   c.bpc = p->bpc;
-  return launch_plan(p->args, p->dtype, c, p->mean_n, p->device, s);
+  return launch_plan(p->args, p->dtype, c, p->mean_n, p->device, s, plan_pol(p->peer));
 }
 
 int reduce_via_table(int dtype, const Cfg &c, void *out, const void *const *in, int n, size_t count,
@@ -1688,6 +1749,17 @@ int hiccl_reduce_plan_set_engine(hiccl_reduce_plan_t *p, int engine) {
   p->dirty = true;
   return 0;
 }
+
+int hiccl_reduce_plan_set_peer(hiccl_reduce_plan_t *p, int flags) {
+  if (!p) return fail(hipErrorInvalidValue, "plan_set_peer: plan is NULL");
+  if (flags & ~(HICCL_PEER_STORES | HICCL_PEER_LOADS))
+    return fail(hipErrorInvalidValue, "plan_set_peer: flags must be a combination of HICCL_PEER_STORES and HICCL_PEER_LOADS");
+  p->peer = flags;
+  p->dirty = true;
+  return 0;
+}
+
+int hiccl_reduce_plan_peer(const hiccl_reduce_plan_t *p) { return p ? p->peer : -1; }
 
 int hiccl_reduce_plan_set_config(hiccl_reduce_plan_t *p, const hiccl_reduce_config_t *cfg) {
   if (!p) return fail(hipErrorInvalidValue, "plan_set_config: plan is NULL");
@@ -2048,6 +2120,7 @@ struct hiccl_program {
     std::vector<const void *> in;
     size_t count;
     bool bytes;  // exact byte copy (a HICCL_BYTES plan's compute)
+    int peer;    // the plan's hiccl_reduce_plan_set_peer flags
   };
   std::vector<Unit> units;  // the unit batch (after the phases)
   struct Phase {
@@ -2142,7 +2215,7 @@ int prog_upload(hiccl_program *p, hipStream_t s) {
     d.head = sp.head;
     d.tail = sp.tail;
     d.n = (uint32_t)u.in.size();
-    d.pad = u.bytes ? 1u : 0u;
+    d.pad = (u.bytes ? 1u : 0u) | ((uint32_t)u.peer << 1);
     d.tile_begin = unit_comp.size();
     for (size_t k = 0; k < u.in.size(); k++) ptrs[c * maxn + k] = u.in[k];
     const uint64_t nt = tiles_for(sp.npkt, unit);
@@ -2250,7 +2323,7 @@ int hiccl_program_add_plan(hiccl_program_t *p, const hiccl_reduce_plan_t *plan) 
     return fail(hipErrorInvalidValue, "program_add_plan: the plan's dtype is neither the program's nor HICCL_BYTES");
   if (plan->req.acc == HICCL_ACC_WIDE)
     return fail(hipErrorInvalidValue, "program_add_plan: programs accumulate natively (HICCL_ACC_NATIVE) only");
-  for (auto &c : plan->comps) p->units.push_back(hiccl_program::Unit{c.out, c.in, c.count, bytes});
+  for (auto &c : plan->comps) p->units.push_back(hiccl_program::Unit{c.out, c.in, c.count, bytes, plan->peer});
   p->dirty = true;
   return 0;
 }

@@ -101,10 +101,14 @@ std::vector<std::list<Command<T>>> instantiate(const std::vector<std::vector<Col
         comm->add(x.sendbuf, x.sendoffset, x.recvbuf, x.recvoffset, x.count, x.sendid, x.recvid, fuse && x.feeds);
       for (auto &c : step[i].comps) {
         std::vector<T *> in = c.inputs;
+        bool peer = false;  // an input read in place from a peer's buffer
         if (fuse && c.compid == CommBench::myid)
           for (auto &p : in)
-            if (T *remote = comm->fused_source(p)) p = remote;
-        comp->add(in, c.output, c.count, c.compid);
+            if (T *remote = comm->fused_source(p)) {
+              p = remote;
+              peer = true;
+            }
+        comp->add(in, c.output, c.count, c.compid, peer);
       }
       pipeline[i].emplace_back(comm, comp);
     }

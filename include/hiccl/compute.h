@@ -105,7 +105,10 @@ class Compute {
   Compute &operator=(const Compute &) = delete;
 
   // compute.h:47-85.  Every rank calls add; the owning rank records.
-  void add(std::vector<T *> &in, T *out, size_t n, int compid) {
+  // `peer_inputs`: some input is a peer GPU's buffer read in place (fused
+  // gather): the step's kernel then loads with system scope
+  // (hiccl_reduce_plan_set_peer).
+  void add(std::vector<T *> &in, T *out, size_t n, int compid, bool peer_inputs = false) {
     if (CommBench::myid != compid) return;
     inputbuf.push_back(in);
     outputbuf.push_back(out);
@@ -123,7 +126,11 @@ class Compute {
         check(hiccl_reduce_plan_set_engine(plan, eng), "plan_set_engine");
       }
     }
+    if (peer_inputs && !(hiccl_reduce_plan_peer(plan) & HICCL_PEER_LOADS))
+      check(hiccl_reduce_plan_set_peer(plan, hiccl_reduce_plan_peer(plan) | HICCL_PEER_LOADS), "plan_set_peer");
     check(hiccl_reduce_plan_add(plan, out, (const void *const *)in.data(), (int)in.size(), n), "plan_add");
+#else
+    (void)peer_inputs;
 #endif
   }
 

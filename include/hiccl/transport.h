@@ -1233,7 +1233,15 @@ class Comm {
       const bool move = x.sendid != x.recvid && !x.fused && (lib == IPC || lib == IPC_get) && myid == mover_of(x);
       if (!self && !move) continue;
       hiccl_reduce_plan_t *&p = self ? selfplan : moveplan;
-      if (!p && hiccl_reduce_plan_create(&p, HICCL_BYTES, mydevice)) die("transport", hiccl_last_error());
+      if (!p) {
+        if (hiccl_reduce_plan_create(&p, HICCL_BYTES, mydevice)) die("transport", hiccl_last_error());
+        // a put writes the peer's buffer, a get reads it: system-scope
+        // stores / loads, so the bytes are in the peer's HBM when the done
+        // token says so and no stale line of it is read back
+        // (hiccl_reduce_plan_set_peer)
+        if (!self && hiccl_reduce_plan_set_peer(p, lib == IPC ? HICCL_PEER_STORES : HICCL_PEER_LOADS))
+          die("transport", hiccl_last_error());
+      }
       const void *src = self || lib == IPC ? (const void *)x.src : (const void *)x.remote;
       void *dst = self || lib == IPC_get ? (void *)x.dst : (void *)x.remote;
       if (lib == IPC && !self) dst = x.remote;

@@ -184,6 +184,29 @@ int hiccl_reduce_plan_set_engine(hiccl_reduce_plan_t *plan, int engine);
  * are nt.  Anything else is refused with hipErrorInvalidValue -- no field is
  * silently ignored. */
 int hiccl_reduce_plan_set_config(hiccl_reduce_plan_t *plan, const hiccl_reduce_config_t *cfg);
+/* Peer memory.  The transport's data movement (the CommBench IPC put / get
+ * the reference registers at command.h:122,132 and starts at comm.h:190,197)
+ * and the fused gather + reduce (reduce.h:134-170's receive buffers read in
+ * place) run plans whose outputs or inputs live in ANOTHER GPU's memory
+ * (HIP IPC mappings over xGMI).  Their launches must hand bytes to, or take
+ * them from, a kernel of the other GPU in the same stream-ordered pipeline,
+ * with only a device-side flag in between:
+ *   HICCL_PEER_STORES  every store is system-scope write-through (nothing of
+ *                      a peer's buffer stays dirty in this GPU's L2s after
+ *                      the kernel);
+ *   HICCL_PEER_LOADS   every load is system-scope coherent (no L2 line of a
+ *                      peer's buffer cached by an earlier launch is served).
+ * Same results; runs the PHASE engine's default shape and TILE at unroll 4
+ * (f32 / bf16 also 2): an automatic wide-tile choice becomes unroll 4, an
+ * explicit unroll the peer kernels lack fails at launch.  Kept by
+ * hiccl_program_add_plan for the plan's computes. */
+typedef enum {
+  HICCL_PEER_STORES = 1,
+  HICCL_PEER_LOADS = 2
+} hiccl_peer_t;
+int hiccl_reduce_plan_set_peer(hiccl_reduce_plan_t *plan, int flags);
+/* The plan's peer flags (-1 for NULL). */
+int hiccl_reduce_plan_peer(const hiccl_reduce_plan_t *plan);
 /* The engine the last upload resolved to (TILE before the first launch). */
 int hiccl_reduce_plan_engine(const hiccl_reduce_plan_t *plan);
 int hiccl_reduce_plan_add(hiccl_reduce_plan_t *plan, void *out, const void *const *in, int n,

@@ -43,13 +43,17 @@ def _inorder(xs):
     return acc
 
 
+@pytest.mark.parametrize("peer", ["none", "put", "get"])
 @pytest.mark.parametrize("count", [(1 << 18) + 3, (1 << 24) + 5], ids=["half_tiles", "full_tiles"])
-def test_units_wait_for_the_phases(count):
+def test_units_wait_for_the_phases(count, peer):
     """The program waits for a flag; another stream first rewrites the copy's
     source, then sets the flag: the copy (and the reduction of the same
     batch) must see the new source -- no unit ran before the gate opened.
     Three launches with new contents each time; the program is capped at 64
-    workgroups so the other stream's kernels always find room on the GPU."""
+    workgroups so the other stream's kernels always find room on the GPU.
+    `peer`: the transport's peer policies carried into the program (an IPC
+    put's system-scope stores or a get's system-scope loads for the copy,
+    the fused gather's system-scope loads for the reduction)."""
     src = torch.empty(count, device=DEV)
     b = torch.empty(count, device=DEV)
     hiccl_amd.fill_uniform(b, 7, 1)
@@ -60,6 +64,9 @@ def test_units_wait_for_the_phases(count):
     f = flags.data_ptr()
     cp = _copy_plan(dst, src, count * 4)
     red = _sum_plan(out, [src, b], count)
+    if peer != "none":
+        cp.set_peer(L.HICCL_PEER_STORES if peer == "put" else L.HICCL_PEER_LOADS)
+        red.set_peer(L.HICCL_PEER_LOADS)
     prog = hiccl_amd.Program(torch.float32, device=0)
     prog.add_signal([], [f])
     prog.add_plan(cp)

@@ -768,6 +768,96 @@ def test_plan_config_same_bits(oracle, cfg, dtype):
     comp.close()
 
 
+@pytest.mark.parametrize("peer", [1, 2, 3], ids=["stores", "loads", "both"])
+@pytest.mark.parametrize("dtype,cfg", [(np.float32, None), (np.float32, dict(engine=2)),
+                                       (np.float32, dict(engine=1, unroll=2)), (np.uint16, None),
+                                       (np.float64, None), (np.uint64, dict(engine=2))],
+                         ids=["f32", "f32-phase", "f32-u2", "bf16", "f64", "u64-phase"])
+def test_plan_peer_policy_same_bits(oracle, peer, dtype, cfg):
+    """hiccl_reduce_plan_set_peer (system-scope stores / loads for buffers in
+    another GPU's memory, the transport's puts and gets and the fused
+    gather): the same bits as the oracle on a ragged, misaligned batch (the
+    scalar head/tail path with its fences included), relaunched."""
+    rng = np.random.default_rng(11)
+    tdt = TORCH_OF[np.dtype(dtype)]
+    comp = hiccl_amd.Compute(tdt, device=0, config=cfg)
+    comp.set_peer(peer)
+    assert comp.peer() == peer
+    outs, exps, keep = [], [], []
+    for c in range(7):
+        n = int(rng.integers(1, 10))
+        count = int(rng.integers(1, 200000))
+        if np.dtype(dtype) == np.uint64:
+            x = rng.integers(0, 1 << 63, (n, count), dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+        else:
+            x = oracle.fill(n, count, seed=90 + c, dtype=dtype)
+        ins = [to_dev(r).view(tdt) for r in x]
+        keep += ins
+        ob = torch.empty(count + 1, dtype=tdt, device=DEV)
+        comp.add(ins, (ob, 1), count, compid=0)
+        outs.append((ob, count))
+        exps.append(oracle.reduce(list(x), dtype=dtype))
+    for _ in range(2):
+        for ob, _c in outs:
+            ob.fill_(0)
+        comp.start()
+        comp.wait()
+        for (ob, count), e in zip(outs, exps):
+            got = to_host(ob[1:1 + count], dtype)
+            assert bits_equal(got, e), (peer, cfg, first_mismatch(got, e))
+    comp.close()
+
+
+@pytest.mark.parametrize("peer", [1, 2])
+def test_byte_copy_plan_peer_policy_exact(peer):
+    """The transport's batched copies with the peer policy it uses (IPC put:
+    system-scope stores; IPC get: system-scope loads): exact at odd sizes and
+    byte offsets."""
+    import ctypes
+    from hiccl_amd import _lib as L
+    lib = L.lib()
+    plan = ctypes.c_void_p()
+    assert lib.hiccl_reduce_plan_create(ctypes.byref(plan), L.HICCL_BYTES, 0) == 0
+    assert lib.hiccl_reduce_plan_set_peer(plan, 7) == 1  # unknown bits refused
+    assert lib.hiccl_reduce_plan_set_peer(plan, peer) == 0
+    rng = np.random.default_rng(peer)
+    src = torch.from_numpy(rng.integers(0, 256, (1 << 21) + 64, dtype=np.uint8)).to(DEV)
+    outs = []
+    for so, do, nb in ((0, 0, 1 << 20), (1, 3, 4099), (5, 0, 17), (13, 11, (1 << 21) - 5)):
+        dst = torch.zeros(nb + 64, dtype=torch.uint8, device=DEV)
+        tab = (ctypes.c_void_p * 1)(src.data_ptr() + so)
+        assert lib.hiccl_reduce_plan_add(plan, ctypes.c_void_p(dst.data_ptr() + do), tab, 1, nb) == 0, L.last_error()
+        outs.append((dst, so, do, nb))
+    assert lib.hiccl_reduce_plan_launch(plan, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+    torch.cuda.synchronize()
+    s = src.cpu().numpy()
+    for dst, so, do, nb in outs:
+        d = dst.cpu().numpy()
+        assert np.array_equal(d[do:do + nb], s[so:so + nb])
+        assert not d[:do].any() and not d[do + nb:].any()
+    lib.hiccl_reduce_plan_destroy(plan)
+
+
+def test_plan_peer_policy_replaces_wide_tiles(oracle):
+    """Two f32 inputs of 1 GiB would take wide tiles (unroll 16), which the
+    peer kernels lack: with a peer policy the plan runs TILE at unroll 4,
+    sampled-exact."""
+    n, count, seed = 2, 1 << 28, 515
+    ins = [torch.empty(count, device=DEV) for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, seed, k)
+    out = torch.empty(count, device=DEV)
+    comp = hiccl_amd.Compute(torch.float32, device=0)
+    comp.set_peer(2)
+    comp.add(ins, out, count, compid=0)
+    comp.start()
+    comp.wait()
+    assert comp.engine() == hiccl_amd.HICCL_ENGINE_TILE
+    ok, msg = _sampled(out, n, count, seed)
+    assert ok, msg
+    comp.close()
+
+
 def test_plan_config_refuses_unsupported_fields():
     for bad in (dict(engine=1, unroll=32), dict(engine=1, unroll=3), dict(engine=2, unroll=4), dict(engine=1, block=512),
                 dict(nontemporal=1), dict(store_policy=3), dict(drain=1), dict(schedule=7)):
