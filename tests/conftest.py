@@ -19,6 +19,12 @@ REF_SO = os.path.join(ROOT, "oracle", "_ref", "libhiccl_ref.so")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    config.addinivalue_line("markers", "runtime_probe: records the HIP runtime's behaviour; runs after every "
+                                       "other test, so that under -x it never keeps the parity tests from running")
+
+
+def pytest_collection_modifyitems(config, items):
+    items.sort(key=lambda it: it.get_closest_marker("runtime_probe") is not None)  # stable: order kept otherwise
 
 
 def _build_oracle():

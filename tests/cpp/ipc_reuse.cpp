@@ -47,6 +47,7 @@ struct Export {
   hipIpcMemHandle_t h;
   uint64_t addr;
   uint64_t nonce;
+  uint64_t ok;  // 0: hipIpcGetMemHandle failed (recorded; peers skip it)
 };
 
 // read the first 8 bytes of `p` with the copy engine and with a kernel;
@@ -69,15 +70,22 @@ static uint64_t next_nonce(int me) {
   return seq;
 }
 
-// this rank's nbuf fresh allocations with nonces; every rank's exports
-static std::vector<void *> alloc_and_export(size_t bytes, int nbuf, int me, int np, std::vector<Export> &all) {
+// this rank's nbuf fresh allocations with nonces; every rank's exports.  A
+// failed export is counted in *failed (an outcome this program records, like
+// a failed open) and marked, so the peers do not open it.
+static std::vector<void *> alloc_and_export(size_t bytes, int nbuf, int me, int np, std::vector<Export> &all,
+                                            long *failed) {
   std::vector<void *> a(nbuf);
   std::vector<Export> mine(nbuf);
   for (int j = 0; j < nbuf; j++) {
     check(hipMalloc(&a[j], bytes), "hipMalloc");
     mine[j].nonce = next_nonce(me);
     check(hipMemcpy(a[j], &mine[j].nonce, 8, hipMemcpyHostToDevice), "write nonce");
-    check(hipIpcGetMemHandle(&mine[j].h, a[j]), "export");
+    mine[j].ok = hipIpcGetMemHandle(&mine[j].h, a[j]) == hipSuccess;
+    if (!mine[j].ok) {
+      (void)hipGetLastError();
+      (*failed)++;
+    }
     mine[j].addr = (uint64_t)(uintptr_t)a[j];
   }
   check(hipDeviceSynchronize(), "sync");
@@ -111,16 +119,18 @@ int main(int argc, char **argv) {
         const std::string v = variant;
         const bool do_close = v == "close" || (v == "mixed" && me % 2 == 0);
         const bool late = v == "late";
-        // B reads, A ok, recycled, B copy ok, B kernel ok, late reads, late ok, A opens, A open failed, B open failed
-        long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        // B reads, A ok, recycled, B copy ok, B kernel ok, late reads, late ok, A opens, A open failed,
+        // B open failed, A export failed, B export failed
+        long st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         std::vector<void *> kept;
         for (int r = 0; r < rounds; r++) {
           std::vector<Export> ea, eb;
-          std::vector<void *> a = alloc_and_export(bytes, nbuf, me, np, ea);  // 1.
+          std::vector<void *> a = alloc_and_export(bytes, nbuf, me, np, ea, &st[10]);  // 1.
           std::vector<void *> ma;
           for (int p = 0; p < np; p++)  // 2.
             for (int j = 0; j < nbuf && p != me; j++) {
               const Export &e = ea[(size_t)p * nbuf + j];
+              if (!e.ok) continue;
               void *m = nullptr;
               st[7]++;
               if (hipIpcOpenMemHandle(&m, e.h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
@@ -137,12 +147,13 @@ int main(int argc, char **argv) {
           }
           MPI_Barrier(MPI_COMM_WORLD);
           for (void *p : a) check(hipFree(p), "free A");  // 3.
-          std::vector<void *> b = alloc_and_export(bytes, nbuf, me, np, eb);
+          std::vector<void *> b = alloc_and_export(bytes, nbuf, me, np, eb, &st[11]);
           std::vector<void *> mb;
           std::vector<uint64_t> nb;
           for (int p = 0; p < np; p++)  // 4.
             for (int j = 0; j < nbuf && p != me; j++) {
               const Export &f = eb[(size_t)p * nbuf + j];
+              if (!f.ok) continue;
               for (int i = 0; i < nbuf; i++)
                 if (f.addr == ea[(size_t)p * nbuf + i].addr) st[2]++;
               void *m = nullptr;
@@ -171,16 +182,17 @@ int main(int argc, char **argv) {
           MPI_Barrier(MPI_COMM_WORLD);
         }
         for (void *m : kept) check(hipIpcCloseMemHandle(m), "close kept");
-        long tot[10];
-        MPI_Reduce(st, tot, 10, MPI_LONG, MPI_SUM, 0, MPI_COMM_WORLD);
+        long tot[12];
+        MPI_Reduce(st, tot, 12, MPI_LONG, MPI_SUM, 0, MPI_COMM_WORLD);
         if (me == 0)
           std::printf("{\"variant\": \"%s\", \"ranks\": %d, \"bytes\": %zu, \"buffers\": %d, \"rounds\": %d, "
                       "\"devices\": %d, \"first_opens\": %ld, \"first_open_failed\": %ld, \"first_mapping_ok\": %ld, "
                       "\"reads\": %ld, \"second_open_failed\": %ld, \"recycled_address\": %ld, "
                       "\"second_mapping_copy_engine_ok\": %ld, \"second_mapping_kernel_ok\": %ld, "
-                      "\"late_close_reads\": %ld, \"after_late_close_ok\": %ld}\n",
+                      "\"late_close_reads\": %ld, \"after_late_close_ok\": %ld, \"first_export_failed\": %ld, "
+                      "\"second_export_failed\": %ld}\n",
                       variant, np, bytes, nbuf, rounds, ndev, tot[7], tot[8], tot[1], tot[0], tot[9], tot[2], tot[3],
-                      tot[4], tot[5], tot[6]);
+                      tot[4], tot[5], tot[6], tot[10], tot[11]);
         std::fflush(stdout);
         MPI_Barrier(MPI_COMM_WORLD);
       }
