@@ -4,8 +4,8 @@ A program is ONE launch of signal/wait phases followed by a batch of
 independent computes (exact byte copies from HICCL_BYTES plans, reductions
 of the program's dtype); HiCCL::Comm records its stream-ordered pipeline as
 a list of them.  The checks: no unit starts before the
-last phase is satisfied (a peer-like stream writes the source and then the
-flag while the program waits), consecutive programs see each other's
+last phase is satisfied (the host, as the peer, checks nothing was copied,
+writes the source and then the flag while the program waits), consecutive programs see each other's
 results, phases store / await their per-launch epochs (and epoch +
 *epoch_dev under graph replay), relaunches reuse the gate word, a wait that
 is never satisfied times out with the error word set while the grid still
@@ -43,50 +43,79 @@ def _inorder(xs):
     return acc
 
 
+def _host_coherent(nbytes):
+    """Fine-grained (coherent) pinned host memory, mapped for the GPU at the
+    same address: the host can play the peer -- its stores reach the waiting
+    kernel with no GPU queue involved (hipHostMallocCoherent | Mapped)."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    p = ctypes.c_void_p()
+    assert hip.hipHostMalloc(ctypes.byref(p), ctypes.c_size_t(nbytes), ctypes.c_uint(0x40000000 | 0x2)) == 0
+    return p.value, (lambda: hip.hipHostFree(p))
+
+
 @pytest.mark.parametrize("peer", ["none", "put", "get"])
-@pytest.mark.parametrize("count", [(1 << 18) + 3, (1 << 24) + 5], ids=["half_tiles", "full_tiles"])
+@pytest.mark.parametrize("count", [(1 << 18) + 3, (1 << 22) + 5], ids=["half_tiles", "full_tiles"])
 def test_units_wait_for_the_phases(count, peer):
-    """The program waits for a flag; another stream first rewrites the copy's
-    source, then sets the flag: the copy (and the reduction of the same
-    batch) must see the new source -- no unit ran before the gate opened.
-    Three launches with new contents each time; the program is capped at 64
-    workgroups so the other stream's kernels always find room on the GPU.
-    `peer`: the transport's peer policies carried into the program (an IPC
-    put's system-scope stores or a get's system-scope loads for the copy,
-    the fused gather's system-scope loads for the reduction)."""
-    src = torch.empty(count, device=DEV)
+    """The program waits for a flag; the host plays the peer: while the
+    program waits it checks that no copy unit has written yet, rewrites the
+    copy's source, then sets the flag -- the copy (and the reduction of the
+    same batch) must see the new source: no unit ran before the gate opened.
+    Source, copy destination and flag live in coherent pinned host memory,
+    so the peer needs no GPU queue (a second stream of this process may share
+    the program's hardware queue and then waits behind it).  Three launches
+    with new contents each time.  `peer`: the transport's peer policies
+    carried into the program (an IPC put's system-scope stores or a get's
+    system-scope loads for the copy, the fused gather's system-scope loads
+    for the reduction)."""
+    import time
+    nb = count * 4
+    sp, free_s = _host_coherent(nb)
+    dp, free_d = _host_coherent(nb)
+    fp, free_f = _host_coherent(256)
+    src_np = np.ctypeslib.as_array((ctypes.c_float * count).from_address(sp))
+    dst_np = np.ctypeslib.as_array((ctypes.c_float * count).from_address(dp))
+    flag_np = np.ctypeslib.as_array((ctypes.c_int32 * 64).from_address(fp))
+    flag_np[:] = 0
+    src = torch.from_numpy(src_np)  # host tensors: the plans only take their addresses
+    dst = torch.from_numpy(dst_np)
     b = torch.empty(count, device=DEV)
     hiccl_amd.fill_uniform(b, 7, 1)
-    dst = torch.full((count,), float("nan"), device=DEV)
     out = torch.empty(count, device=DEV)
-    flags = torch.zeros(4, dtype=torch.int32, device=DEV)
     err = torch.zeros(1, dtype=torch.int32, device=DEV)
-    f = flags.data_ptr()
-    cp = _copy_plan(dst, src, count * 4)
+    cp = _copy_plan(dst, src, nb)
     red = _sum_plan(out, [src, b], count)
     if peer != "none":
         cp.set_peer(L.HICCL_PEER_STORES if peer == "put" else L.HICCL_PEER_LOADS)
         red.set_peer(L.HICCL_PEER_LOADS)
     prog = hiccl_amd.Program(torch.float32, device=0)
-    prog.add_signal([], [f])
+    prog.add_signal([], [fp])
     prog.add_plan(cp)
     prog.add_plan(red)
-    prog.set_max_workgroups(64)
     assert prog.units() == 2 and prog.phases() == 1
-    other = torch.cuda.Stream()
-    tab = (ctypes.c_void_p * 1)(f)
-    for it in range(3):
-        hiccl_amd.fill_uniform(src, 100 + it, 0)
+    rng = np.random.default_rng(count)
+    try:
+        for it in range(3):
+            src_np[:] = rng.standard_normal(count, dtype=np.float32)
+            dst_np[:] = np.nan
+            prog.launch([it + 1], err=err.data_ptr(), timeout_s=20.0)
+            time.sleep(0.05)
+            assert np.isnan(dst_np).all(), f"launch {it}: a copy unit ran before the gate opened"
+            new = rng.standard_normal(count, dtype=np.float32)
+            src_np[:] = new  # the "peer": new data, then the token
+            flag_np[0] = it + 1
+            torch.cuda.synchronize()
+            assert err.item() == 0
+            assert np.array_equal(dst_np.view(np.int32), new.view(np.int32)), f"launch {it}: stale source copied"
+            exp = torch.from_numpy(new).to(DEV)
+            assert torch.equal(out.view(torch.int32), _inorder([exp, b]).view(torch.int32))
+    finally:
         torch.cuda.synchronize()
-        prog.launch([it + 1], err=err.data_ptr(), timeout_s=20.0)
-        hiccl_amd.fill_uniform(src, 200 + it, 0, stream=other)  # the "peer": new data, then the token
-        L.check(L.lib().hiccl_signal_wait(tab, 1, None, 0, it + 1, None, 5.0, ctypes.c_void_p(other.cuda_stream)),
-                "signal_wait")
-        torch.cuda.synchronize()
-        assert err.item() == 0
-        assert torch.equal(dst.view(torch.int32), src.view(torch.int32)), f"launch {it}: a unit ran early"
-        assert torch.equal(out.view(torch.int32), _inorder([src, b]).view(torch.int32))
-    prog.close()
+        prog.close()
+        cp.close()
+        red.close()
+        free_s()
+        free_d()
+        free_f()
 
 
 def test_chain_of_programs():
