@@ -560,6 +560,8 @@ def main():
     ap.add_argument("--chunks", action="store_true")
     ap.add_argument("--roundtrip", action="store_true")
     ap.add_argument("--progstep", action="store_true", help="one C5 step: separate launches vs one step program")
+    ap.add_argument("--stepscale", action="store_true",
+                    help="the C5 step's batched kernel scaled 1/8x..16x: fixed cost + bytes / rate fit")
     ap.add_argument("--c2variants", action="store_true")
     ap.add_argument("--crossover", action="store_true")
     ap.add_argument("--planvs", action="store_true")
@@ -611,6 +613,8 @@ def main():
         return roundtrip(args)
     if args.progstep:
         return progstep(args)
+    if args.stepscale:
+        return stepscale(args)
 
     n, count = args.n, 1 << args.log2count
     cfg = None
@@ -1071,6 +1075,62 @@ def progstep(args):
     print(json.dumps(row), flush=True)
     for pr in (p_copy, p_comp, p_tail, q_copy, q_comp):
         pr.close()
+    return 0
+
+
+def stepscale(args):
+    """The C5 step's batched reduction (4 computes of n = 2 and one of n = 4,
+    2^18 f32 each at scale 1) at scales 1/8 ... 16, one
+    plan launch each, queued GPU time per launch (events around 200
+    back-to-back launches), interleaved rounds.  A least-squares fit
+    t = t0 + bytes / rate over the scales splits a launch into a fixed part
+    (dispatch, first-byte latency, drain) and a bandwidth part; at scale 1
+    it says how far the step kernel is from its HBM roofline and why."""
+    scales = (0.125, 0.25, 0.5, 1, 2, 4, 8, 16)
+    base = 1 << 18
+    dev = torch.cuda.current_device()
+    cases = {}
+    keep = []
+    for f in scales:
+        c = int(base * f)
+        bufs = [torch.empty(c, device="cuda") for _ in range(12)]
+        for k, t in enumerate(bufs):
+            hiccl_amd.fill_uniform(t, SEED, k)
+        outs = [torch.empty(c, device="cuda") for _ in range(5)]
+        comp = hiccl_amd.Compute(torch.float32, device=dev)
+        for j in range(4):
+            comp.add([bufs[2 * j], bufs[2 * j + 1]], outs[j], c, compid=0)
+        comp.add(bufs[8:12], outs[4], c, compid=0)
+        keep.append((bufs, outs))
+        cases[f] = (comp, 17 * c * 4)  # 12 inputs read + 5 outputs written
+    stream = torch.cuda.current_stream()
+    res = {f: [] for f in scales}
+    for _ in range(5):
+        for f in scales:
+            comp = cases[f][0]
+            res[f].append(time_queued(lambda: comp.enqueue(stream), 200, 10) * 1e3)
+    xs = np.array([cases[f][1] for f in scales], dtype=np.float64)
+    ys = np.array([float(np.median(res[f])) for f in scales])  # us
+    A = np.vstack([np.ones_like(xs), xs]).T
+    (t0, slope), *_ = np.linalg.lstsq(A, ys, rcond=None)
+    rate_GBps = (1.0 / slope) * 1e6 / 1e9  # slope: us per byte
+    rows = [{"scale": f, "algorithmic_bytes": int(cases[f][1]), "queued_us": round(float(y), 3),
+             "GBps": round(cases[f][1] / y * 1e6 / 1e9, 1), "fit_us": round(float(t0 + slope * cases[f][1]), 3)}
+            for f, y in zip(scales, ys)]
+    ok = True
+    for f in scales:
+        bufs, outs = keep[scales.index(f)]
+        ref = torch.empty_like(outs[0])
+        hiccl_amd.reduce(ref, [bufs[0], bufs[1]])
+        ok = ok and torch.equal(ref.view(torch.int32), outs[0].view(torch.int32))
+    torch.cuda.synchronize()
+    one = rows[scales.index(1)]
+    print(json.dumps({"mode": "stepscale", "shape": "4 x (n=2) + 1 x (n=4) computes of scale x 2^18 f32, one plan launch",
+                      "rows": rows, "fit_fixed_us": round(float(t0), 3), "fit_rate_GBps": round(rate_GBps, 1),
+                      "scale1_fixed_share": round(float(t0) / one["queued_us"], 3),
+                      "scale1_frac_of_8TBps": round(one["GBps"] / 8000.0, 3), "bits_ok": bool(ok)}), flush=True)
+    for comp, _ in cases.values():
+        comp.close()
     return 0
 
 
