@@ -1115,8 +1115,24 @@ def stepscale(args):
     (t0, slope), *_ = np.linalg.lstsq(A, ys, rcond=None)
     rate_GBps = (1.0 / slope) * 1e6 / 1e9  # slope: us per byte
     rows = [{"scale": f, "algorithmic_bytes": int(cases[f][1]), "queued_us": round(float(y), 3),
-             "GBps": round(cases[f][1] / y * 1e6 / 1e9, 1), "fit_us": round(float(t0 + slope * cases[f][1]), 3)}
+             "GBps": round(cases[f][1] / y * 1e6 / 1e9, 1), "fit_us": round(float(t0 + slope * cases[f][1]), 3),
+             "engine": cases[f][0].engine()}
             for f, y in zip(scales, ys)]
+    # the same launches with the engine / occupancy pinned (what AUTO chose
+    # against the alternatives, per scale)
+    variants = {"tile": dict(engine=1), "tile_bpc2": dict(engine=1, blocks_per_cu=2),
+                "tile_bpc4": dict(engine=1, blocks_per_cu=4), "phase": dict(engine=2)}
+    for name, cfg in variants.items():
+        vt = {f: [] for f in scales}
+        for _ in range(3):
+            for f in scales:
+                comp = cases[f][0]
+                comp.set_config(cfg)
+                vt[f].append(time_queued(lambda: comp.enqueue(stream), 200, 10) * 1e3)
+        for r, f in zip(rows, scales):
+            r[name + "_us"] = round(float(np.median(vt[f])), 3)
+    for f in scales:
+        cases[f][0].set_config({})
     ok = True
     for f in scales:
         bufs, outs = keep[scales.index(f)]
