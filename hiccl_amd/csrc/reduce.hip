@@ -1176,7 +1176,27 @@ int auto_engine(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
     if (tickets >= kTileMinTicketsPerWG * (uint64_t)device_cus(dev)) return HICCL_ENGINE_TILE;
   }
   const uint64_t chunk = (uint64_t)kPhBlock * phase_p_dtype(dtype, acc);
-  const uint64_t per_cu = npkt / ((uint64_t)device_cus(dev) * chunk);  // phased chunks per CU
+  const uint64_t cus = (uint64_t)device_cus(dev);
+  const uint64_t per_cu = npkt / (cus * chunk);  // phased chunks per CU
+  if (dtype == HICCL_FLOAT32) {
+    // Round 3, on the round-2 kernels (interleaved one-shot sweep, n = 2 / 3 /
+    // 4 / 8 x 32-144 MiB per input, profiles/r03n_midsize.jsonl; the C5 step
+    // shape scaled up, r03n_stepscale.jsonl): the phased engine needs both
+    // several chunks per CU and whole rounds of them -- one chunk per
+    // workgroup (a CU per workgroup) is a single memory round trip with no
+    // overlap, and a last round that only part of the grid works on (1.25 /
+    // 1.5 / 2.5 chunks per CU) idles the rest: PHASE lost 3-20 % to static
+    // tiles there (n = 3 at 40 MiB: 5.08 vs 6.15 TB/s; the C5 step at 8 x
+    // 2^18: 29.6 vs 23.2 us).  `round_eff` = chunks / (whole rounds x CUs).
+    const uint64_t chunks = (npkt + chunk - 1) / chunk;
+    const double round_eff = chunks ? (double)chunks / (double)(((chunks + cus - 1) / cus) * cus) : 0.0;
+    if (n < 2.5) return per_cu > 16 && round_eff >= 0.89 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
+    if (n < kDynMinInputs) return per_cu >= 4 && round_eff >= 0.89 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
+    // many inputs, under the dynamic tiles' ticket count: PHASE from one
+    // whole chunk per CU unless a third of the last round idles (n = 8 at
+    // 40 MiB: tiles 6.03 vs 5.45; at 48 / 80 MiB PHASE holds: 6.08 / 6.25)
+    return per_cu >= 1 && round_eff >= 0.7 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
+  }
   // two inputs: the static tile order leads from 2 to 16 chunks per CU (f32
   // 64-512 MiB per input: +1-4 %), the phased order below and above it
   // (32 MiB: 5.49 vs 5.17; 1 GiB: 6.13 vs 5.96 TB/s; r01g_xover_smalln.jsonl)

@@ -391,19 +391,22 @@ def test_plan_phase_engine(oracle, each):
 
 
 def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
-    """AUTO resolves to TILE with >= 5 inputs from 64 tickets per workgroup
-    (n = 6: two tiles per ticket, 2^27 f32 per input on 256 CUs); otherwise
-    to PHASE once every CU gets a chunk of 128 KiB (f32: 2^23 elements per
-    input), to TILE below -- and for two inputs also at 2-16 chunks per CU
-    (2^24-2^27 f32)."""
+    """f32 AUTO (round 3, profiles/r03n_midsize.jsonl): TILE with >= 5 inputs
+    from 64 tickets per workgroup (n = 6: two tiles per ticket, 2^27 f32 per
+    input on 256 CUs); below that, with >= 5 inputs, PHASE once every CU gets
+    a 128 KiB chunk (2^23 f32 per input) and the last round of chunks keeps
+    >= 70 % of the CUs busy (n = 8 at 1.25 chunks per CU: TILE); with 3-4
+    inputs PHASE from 4 chunks per CU in whole-enough rounds (~90 %),
+    with 2 inputs from 16; TILE otherwise."""
     count = 1 << 23
     a = torch.empty(1 << 27, device=DEV)
     hiccl_amd.fill_uniform(a, 77, 0)
     out = torch.empty(1 << 27, device=DEV)
     P, T = hiccl_amd.HICCL_ENGINE_PHASE, hiccl_amd.HICCL_ENGINE_TILE
-    for cnt, n, expect in ((1 << 27, 6, T), (1 << 26, 6, P), (count, 6, P), (count, 2, P), (1 << 24, 2, T),
-                           (1 << 26, 4, P), (count // 4, 6, T),
-                           (count // 4, 2, T)):
+    for cnt, n, expect in ((1 << 27, 6, T), (1 << 26, 6, P), (count, 6, P), (count, 2, T), (1 << 24, 2, T),
+                           (1 << 26, 4, P), (count // 4, 6, T), (count // 4, 2, T), (count, 4, T),
+                           (count * 5 // 4, 8, T), (count * 3 // 2, 8, P), (count * 9 // 2, 3, P),
+                           (count * 5 // 2, 4, T)):
         comp = hiccl_amd.Compute(torch.float32, device=0)
         comp.add([a] * n, out, cnt, compid=0)
         comp.start()
