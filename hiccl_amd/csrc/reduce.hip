@@ -923,7 +923,11 @@ struct DevInfo {
 std::mutex g_dev_mu;
 DevInfo g_dev[64];
 
+// hiccl_reduce_auto_choice: the CU count AUTO plans for, in place of a device's
+thread_local int t_cus_override = 0;
+
 int device_cus(int dev) {
+  if (t_cus_override > 0) return t_cus_override;
   if (dev < 0 || dev >= 64) return 256;
   std::lock_guard<std::mutex> lk(g_dev_mu);
   if (g_dev[dev].cus == 0) {
@@ -1005,14 +1009,18 @@ bool per_thread_stream(hipStream_t s) { return s == hipStreamPerThread; }
 // 6.3-6.7 TB/s on C2); never during stream capture (a replayed graph could
 // run beside other work on the same stream's counter) nor on
 // hipStreamPerThread; NULL also on any allocation failure.
+// The schedule rule itself (stream aside).
+bool wants_dynamic(int engine, double n, uint64_t units, uint64_t grid, int schedule, uint32_t grab, int unroll) {
+  if (schedule == HICCL_SCHED_STATIC) return false;
+  if (schedule == HICCL_SCHED_AUTO && (engine != HICCL_ENGINE_TILE || (n < kDynMinInputs && unroll < kWideUnroll)))
+    return false;
+  if (!grab) grab = default_grab(engine, n, unroll);
+  return (units + grab - 1) / grab >= kDynMinUnitsPerWG * grid;
+}
+
 uint32_t *unit_sched_for(int engine, double n, uint64_t units, uint64_t grid, int dev, hipStream_t s,
                          int schedule = HICCL_SCHED_AUTO, uint32_t grab = 0, int unroll = 4 /* kDefUnroll */) {
-  if (schedule == HICCL_SCHED_STATIC) return nullptr;
-  if (schedule == HICCL_SCHED_AUTO &&
-      (engine != HICCL_ENGINE_TILE || (n < kDynMinInputs && unroll < kWideUnroll)))
-    return nullptr;
-  if (!grab) grab = default_grab(engine, n, unroll);
-  if ((units + grab - 1) / grab < kDynMinUnitsPerWG * grid) return nullptr;
+  if (!wants_dynamic(engine, n, units, grid, schedule, grab, unroll)) return nullptr;
   if (per_thread_stream(s) || capturing(s, true)) return nullptr;
   std::lock_guard<std::mutex> lk(g_sched_mu);
   auto it = g_sched.find(SchedKey{dev, s});
@@ -1195,8 +1203,12 @@ int auto_engine(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
     if (n < kDynMinInputs) return per_cu >= 4 && round_eff >= 0.89 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
     // many inputs, under the dynamic tiles' ticket count: PHASE from one
     // whole chunk per CU unless a third of the last round idles (n = 8 at
-    // 40 MiB: tiles 6.03 vs 5.45; at 48 / 80 MiB PHASE holds: 6.08 / 6.25)
-    return per_cu >= 1 && round_eff >= 0.7 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
+    // 40 MiB: tiles 6.03 vs 5.45; at 48 / 80 MiB PHASE holds: 6.08 / 6.25);
+    // from 16 inputs a chunk is >= 2 MiB of reads, and PHASE leads already
+    // with 70 % of the CUs holding one (24 MiB per input, 0.75 chunks per CU:
+    // n = 16 / 32 PHASE 6.56 / 6.34 vs tiles 6.15-6.25; at 0.5 per CU tiles
+    // lead: 6.21 / 6.25 vs 5.43 / 5.61; profiles/r03q_sweep_manyn.jsonl)
+    return (per_cu >= 1 || n >= 16) && round_eff >= 0.7 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
   }
   // two inputs: the static tile order leads from 2 to 16 chunks per CU (f32
   // 64-512 MiB per input: +1-4 %), the phased order below and above it
@@ -1530,6 +1542,30 @@ int hiccl_reduce_f32(float *out, const float *const *in, int n, size_t count, vo
 int hiccl_reduce_bf16(uint16_t *out, const uint16_t *const *in, int n, size_t count,
                       void *stream) {
   return hiccl_reduce_ex(HICCL_BFLOAT16, out, (const void *const *)in, n, count, stream, nullptr);
+}
+
+int hiccl_reduce_auto_choice(int dtype, int acc, size_t count, double n, int cus, int *engine, int *unroll,
+                             int *blocks_per_cu, int *dynamic) {
+  const size_t esz = esize(dtype);
+  if (!esz) return fail(hipErrorInvalidValue, "auto_choice: unknown dtype");
+  if (acc != HICCL_ACC_NATIVE && acc != HICCL_ACC_WIDE) return fail(hipErrorInvalidValue, "auto_choice: bad acc");
+  if (cus <= 0 || n < 0) return fail(hipErrorInvalidValue, "auto_choice: cus must be > 0 and n >= 0");
+  t_cus_override = cus;  // no device query: the choice for `cus` CUs
+  hiccl_reduce_config_t z;
+  memset(&z, 0, sizeof(z));
+  z.acc = acc;
+  Cfg c = resolve(&z);
+  const uint64_t npkt = (uint64_t)count * esz / kPacket;
+  finish_cfg(c, npkt, n, dtype, -1);
+  const uint64_t units = tiles_for(npkt, (uint64_t)c.block * c.unroll);  // tiles or phased chunks
+  const uint64_t grid = std::min<uint64_t>((uint64_t)cus * c.bpc, units);
+  const bool dyn = wants_dynamic(c.engine, n, units, grid, c.schedule, 0, c.unroll);
+  t_cus_override = 0;
+  if (engine) *engine = c.engine;
+  if (unroll) *unroll = c.unroll;
+  if (blocks_per_cu) *blocks_per_cu = c.bpc;
+  if (dynamic) *dynamic = dyn ? 1 : 0;
+  return 0;
 }
 
 // ---------------------------------------------------------------- plan ----

@@ -147,6 +147,15 @@ typedef struct {
 int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t count,
                     void *stream, const hiccl_reduce_config_t *cfg);
 
+/* What AUTO (engine, TILE unroll / PHASE packets per lane, workgroups per
+ * CU, dynamic unit schedule 1/0) picks for a one-shot call of n inputs of
+ * `count` elements whose output is 16-B aligned, on a GPU of `cus` CUs (no
+ * device is queried: host code and tests can ask; a plan asks with the sum
+ * of its computes' elements and their packet-weighted mean n).  A launch on
+ * a capturing stream or hipStreamPerThread takes the static schedule. */
+int hiccl_reduce_auto_choice(int dtype, int acc, size_t count, double n, int cus, int *engine, int *unroll,
+                             int *blocks_per_cu, int *dynamic);
+
 /* ----------------------------------------------------------------------
  * Persistent plan: the C-ABI counterpart of the reference's Compute<T>
  * (compute.h:26-204).  A plan holds any number of registered computes and

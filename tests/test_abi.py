@@ -130,3 +130,50 @@ def test_program_argument_checks_on_host():
     assert lib.hiccl_program_launch(None, None, None, None, 1.0, None) != 0
     assert lib.hiccl_program_num_units(None) == 0 and lib.hiccl_program_num_phases(None) == 0
     lib.hiccl_program_destroy(None)
+
+
+def _auto(dtype, count, n, cus=256, acc=0):
+    import ctypes
+    lib = L.lib()
+    e, u, b, d = (ctypes.c_int() for _ in range(4))
+    rc = lib.hiccl_reduce_auto_choice(dtype, acc, count, float(n), cus, ctypes.byref(e), ctypes.byref(u),
+                                      ctypes.byref(b), ctypes.byref(d))
+    assert rc == 0, L.last_error()
+    return e.value, u.value, b.value, d.value
+
+
+def test_auto_choice_rule_table_on_host():
+    """hiccl_reduce_auto_choice (no device queried): AUTO's engine / shape /
+    schedule for the BASELINE configs and the round-3 mid-size rule
+    (profiles/r03n_midsize.jsonl, r03q_sweep_manyn.jsonl)."""
+    T, P = L.HICCL_ENGINE_TILE, L.HICCL_ENGINE_PHASE
+    f32, bf16 = L.HICCL_FLOAT32, L.HICCL_BFLOAT16
+    MiB = 1 << 20
+    cases = [  # (dtype, elements per input, n) -> (engine, unroll, blocks per CU, dynamic)
+        ((f32, 1 << 28, 8), (T, 4, 1, 1)),       # C2: tiles on the ticket counter
+        ((f32, 1 << 26, 2), (T, 4, 1, 0)),       # C3, two inputs: static tiles
+        ((f32, 1 << 26, 3), (P, 16, 1, 0)),      # C3, 3-4 inputs: 8 whole chunks per CU
+        ((f32, 1 << 26, 4), (P, 16, 1, 0)),
+        ((f32, 1 << 26, 8), (T, 4, 1, 1)),       # C3, many inputs: 64 tickets per workgroup
+        ((f32, 1 << 26, 64), (T, 4, 1, 1)),
+        ((f32, 1 << 28, 2), (T, 16, 1, 1)),      # 1 GiB per input, few inputs: wide tiles
+        ((f32, 1 << 28, 3), (T, 8, 1, 1)),
+        ((f32, 40 * MiB // 4, 3), (T, 4, 1, 0)),  # 1.25 chunks per CU: tiles
+        ((f32, 32 * MiB // 4, 4), (T, 4, 1, 0)),  # one chunk per CU, 3-4 inputs: tiles
+        ((f32, 40 * MiB // 4, 8), (T, 4, 1, 0)),  # a last round 25 % busy: tiles
+        ((f32, 48 * MiB // 4, 8), (P, 16, 1, 0)),  # 75 % busy: PHASE
+        ((f32, 24 * MiB // 4, 16), (P, 16, 1, 0)),  # 16 inputs, 0.75 chunks per CU: PHASE
+        ((f32, 16 * MiB // 4, 16), (T, 4, 4, 0)),   # 0.5 per CU: tiles, 4 workgroups per CU
+        ((f32, 5 << 18, 2.4), (T, 2, 4, 0)),     # the C5 step's plan: half-size tiles
+        ((bf16, 40 * MiB // 2, 3), (T, 4, 1, 0)),  # bf16 native: the f32 rule
+    ]
+    for (dt, count, n), want in cases:
+        assert _auto(dt, count, n) == want, (dt, count, n, _auto(dt, count, n), want)
+    # bf16 with the wide accumulator keeps the round-2 rule (PHASE from one chunk per CU)
+    assert _auto(bf16, 40 * MiB // 2, 3, acc=L.HICCL_ACC_WIDE)[0] == P
+    # another CU count: the thresholds scale with it
+    assert _auto(f32, 1 << 28, 8, cus=304)[0] == T
+    lib = L.lib()
+    import ctypes
+    assert lib.hiccl_reduce_auto_choice(42, 0, 1024, 2.0, 256, None, None, None, None) == 1
+    assert lib.hiccl_reduce_auto_choice(f32, 0, 1024, 2.0, 0, None, None, None, None) == 1
