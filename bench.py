@@ -1140,11 +1140,19 @@ def stepscale(args):
         hiccl_amd.reduce(ref, [bufs[0], bufs[1]])
         ok = ok and torch.equal(ref.view(torch.int32), outs[0].view(torch.int32))
     torch.cuda.synchronize()
+    # the kernel boundary alone: one 64-lane wave per launch (hiccl_counter_add),
+    # back to back on the same stream
+    ctr = torch.zeros(1, dtype=torch.int32, device="cuda")
+    lib = L.lib()
+    st = ctypes.c_void_p(stream.cuda_stream)
+    empty = [time_queued(lambda: lib.hiccl_counter_add(ctypes.c_void_p(ctr.data_ptr()), 1, st), 200, 10) * 1e3
+             for _ in range(5)]
     one = rows[scales.index(1)]
     print(json.dumps({"mode": "stepscale", "shape": "4 x (n=2) + 1 x (n=4) computes of scale x 2^18 f32, one plan launch",
                       "rows": rows, "fit_fixed_us": round(float(t0), 3), "fit_rate_GBps": round(rate_GBps, 1),
                       "scale1_fixed_share": round(float(t0) / one["queued_us"], 3),
-                      "scale1_frac_of_8TBps": round(one["GBps"] / 8000.0, 3), "bits_ok": bool(ok)}), flush=True)
+                      "scale1_frac_of_8TBps": round(one["GBps"] / 8000.0, 3),
+                      "one_wave_kernel_us": round(float(np.median(empty)), 3), "bits_ok": bool(ok)}), flush=True)
     for comp, _ in cases.values():
         comp.close()
     return 0
