@@ -1147,12 +1147,41 @@ def stepscale(args):
     st = ctypes.c_void_p(stream.cuda_stream)
     empty = [time_queued(lambda: lib.hiccl_counter_add(ctypes.c_void_p(ctr.data_ptr()), 1, st), 200, 10) * 1e3
              for _ in range(5)]
+    # the same 200 launches, and 200 C5-step plan launches (scale 1, static
+    # schedule inside a capture), as ONE hipGraph replay: the boundary
+    # between graph nodes
+    g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    comp1 = cases[1][0]
+    with torch.cuda.stream(side):
+        cs = torch.cuda.current_stream()
+        with torch.cuda.graph(g1, stream=cs):
+            for _ in range(200):
+                lib.hiccl_counter_add(ctypes.c_void_p(ctr.data_ptr()), 1, ctypes.c_void_p(cs.cuda_stream))
+        with torch.cuda.graph(g2, stream=cs):
+            for _ in range(200):
+                comp1.enqueue(cs)
+    graph_us = {}
+    for name, g in (("one_wave_kernel_graph_us", g1), ("scale1_graph_us", g2)):
+        v = []
+        for _ in range(5):
+            g.replay()
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            g.replay()
+            b.record()
+            torch.cuda.synchronize()
+            v.append(a.elapsed_time(b) * 1e3 / 200)
+        graph_us[name] = round(float(np.median(v)), 3)
+    del g1, g2
     one = rows[scales.index(1)]
     print(json.dumps({"mode": "stepscale", "shape": "4 x (n=2) + 1 x (n=4) computes of scale x 2^18 f32, one plan launch",
                       "rows": rows, "fit_fixed_us": round(float(t0), 3), "fit_rate_GBps": round(rate_GBps, 1),
                       "scale1_fixed_share": round(float(t0) / one["queued_us"], 3),
                       "scale1_frac_of_8TBps": round(one["GBps"] / 8000.0, 3),
-                      "one_wave_kernel_us": round(float(np.median(empty)), 3), "bits_ok": bool(ok)}), flush=True)
+                      "one_wave_kernel_us": round(float(np.median(empty)), 3), **graph_us,
+                      "bits_ok": bool(ok)}), flush=True)
     for comp, _ in cases.values():
         comp.close()
     return 0
