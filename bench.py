@@ -1153,6 +1153,8 @@ def stepscale(args):
     g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
     side = torch.cuda.Stream()
     comp1 = cases[1][0]
+    comp1.enqueue(stream)  # re-uploads after the variants' set_config (an upload cannot be captured)
+    torch.cuda.synchronize()
     with torch.cuda.stream(side):
         cs = torch.cuda.current_stream()
         with torch.cuda.graph(g1, stream=cs):
