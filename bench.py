@@ -1057,6 +1057,59 @@ def progstep(args):
     for _ in range(5):
         for k, fn in runs.items():
             res[k].append(time_queued(fn, 200, 10) * 1e3)
+    # The same steps captured into one hipGraph of 200 steps and replayed, as
+    # HICCL_GRAPH=1 runs a pipeline: every phase's epoch is e + *ctr, ctr
+    # bumped by the graph's first node (a kernel boundary between graph
+    # nodes costs less than between eager launches: bench --stepscale).
+    ctr = torch.zeros(1, dtype=torch.int32, device="cuda")
+    cptr = ctypes.c_void_p(ctr.data_ptr())
+    erp = ctypes.c_void_p(err.data_ptr())
+
+    def phase_dev(flag, e, s_):
+        tab = (ctypes.c_void_p * 1)(flag)
+        L.check(lib.hiccl_signal_wait_dev(tab, 1, tab, 1, e, cptr, erp, 10.0, s_), "signal_wait_dev")
+
+    side = torch.cuda.Stream()
+    graphs = {}
+    for name in ("separate_graph", "program_tail_folded_graph", "separate_no_phases_graph",
+                 "program_no_phases_graph"):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            cs = torch.cuda.current_stream()
+            s_ = ctypes.c_void_p(cs.cuda_stream)
+            with torch.cuda.graph(g, stream=cs):
+                L.check(lib.hiccl_counter_add(cptr, 1, s_), "counter_add")
+                for i in range(200):
+                    e = 1000 + i
+                    if name == "separate_graph":
+                        phase_dev(f[0], e, s_)
+                        cp.enqueue(cs)
+                        phase_dev(f[1], e, s_)
+                        comp.enqueue(cs)
+                        phase_dev(f[2], e, s_)
+                    elif name == "program_tail_folded_graph":
+                        p_copy.launch([e], epoch_dev=ctr.data_ptr(), err=err.data_ptr(), timeout_s=10.0, stream=cs)
+                        p_comp.launch([e], epoch_dev=ctr.data_ptr(), err=err.data_ptr(), timeout_s=10.0, stream=cs)
+                    elif name == "separate_no_phases_graph":
+                        cp.enqueue(cs)
+                        comp.enqueue(cs)
+                    else:
+                        q_copy.launch(stream=cs)
+                        q_comp.launch(stream=cs)
+        graphs[name] = g
+    for name, g in graphs.items():
+        v = []
+        for _ in range(5):
+            g.replay()
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            g.replay()
+            b.record()
+            torch.cuda.synchronize()
+            v.append(a.elapsed_time(b) * 1e3 / 200)
+        res[name] = v
+    del graphs
     ref = torch.empty(c, device="cuda")
     ok = True
     for j in range(4):
