@@ -280,7 +280,7 @@ class Comm {
                   steps.size(), libs.size(), streamed ? "stream-ordered" : "host-driven", graphed ? ", graph replay" : "",
                   fused ? ", fused gather" : "", xccl ? ", XCCL on RCCL" : "");
 #ifndef HICCL_PORT_HOST
-    if (programs && CommBench::myid == CommBench::printid) std::printf("step programs: one launch per step\n");
+    if (programs && CommBench::myid == CommBench::printid) std::printf("step programs: token phases folded into the step's launches\n");
 #endif
   }
 

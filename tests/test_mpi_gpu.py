@@ -136,7 +136,7 @@ def test_allreduce_bits_step_program_ab(tmp_path, oracle, np_, count, depth, hie
     rc, out = mpirun(np_, HIP_F32, [8, count, 1, 1, depth, 0, 0, hier, libs, prefix], streamed=True, fused=fused,
                      graph=graph, repeat=4 if graph else 2, extra_env={"HICCL_STEP_PROGRAM": program})
     assert rc == 0, out[-3000:]
-    assert ("step programs: one launch per step" in out) == (program == "1"), out[-2000:]
+    assert ("step programs: token phases folded" in out) == (program == "1"), out[-2000:]
     n = count * np_
     x = {r: oracle.fill(r + 1, n, 1234)[r] for r in range(np_)}
     libmap = {"mpi": S.MPI, "ipc": S.IPC, "ipc_get": S.IPC_GET}
