@@ -566,7 +566,7 @@ def main():
     ap.add_argument("--crossover", action="store_true")
     ap.add_argument("--planvs", action="store_true")
     ap.add_argument("--schedsweep", action="store_true")
-    ap.add_argument("--sweepdtype", default="f32", help="schedsweep: f32 | bf16")
+    ap.add_argument("--sweepdtype", default="f32", help="schedsweep: f32 | bf16 | f64 | u64")
     ap.add_argument("--sweepset", default="", help="schedsweep: '' (schedule/grab) | occupancy")
     ap.add_argument("--xdtype", default="both", help="crossover: f32 | bf16 | both")
     ap.add_argument("--xmib", default="", help="crossover: comma list of MiB per input")
@@ -891,8 +891,8 @@ def schedsweep(args):
                     ("phase_static", dict(engine=2, schedule=1)),
                     ("phase_dyn", dict(engine=2, schedule=2))]
     for n, mib in cases:
-        sdt = torch.bfloat16 if args.sweepdtype == "bf16" else torch.float32
-        esz = 2 if sdt == torch.bfloat16 else 4
+        sdt = {"bf16": torch.bfloat16, "f64": torch.float64, "u64": torch.int64}.get(args.sweepdtype, torch.float32)
+        esz = torch.tensor([], dtype=sdt).element_size()
         count = (mib << 20) // esz
         ins, out = make_bucket(n, count, sdt)
         res = {}
@@ -906,7 +906,13 @@ def schedsweep(args):
             t = float(np.median(v)) * 1e-3
             row[name] = round((n + 1) * count * esz / t / 1e9, 1)
         row["dtype"] = str(sdt).split(".")[-1]
-        row["parity_sample_ok"] = sample_check(out, n, count, bf16=(sdt == torch.bfloat16))
+        if sdt in (torch.float64, torch.int64):  # the in-order sum on the device (f64 adds / u64 wrap-around)
+            acc = torch.zeros_like(out)
+            for t in ins:
+                acc = acc + t
+            row["parity_sample_ok"] = bool(torch.equal(acc.view(torch.int64), out.view(torch.int64)))
+        else:
+            row["parity_sample_ok"] = sample_check(out, n, count, bf16=(sdt == torch.bfloat16))
         print(json.dumps(row), flush=True)
         del ins, out
         torch.cuda.empty_cache()
