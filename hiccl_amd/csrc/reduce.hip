@@ -1186,11 +1186,13 @@ int auto_engine(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
   const uint64_t chunk = (uint64_t)kPhBlock * phase_p_dtype(dtype, acc);
   const uint64_t cus = (uint64_t)device_cus(dev);
   const uint64_t per_cu = npkt / (cus * chunk);  // phased chunks per CU
-  if (dtype == HICCL_FLOAT32 || (dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_NATIVE)) {
+  if (dtype == HICCL_FLOAT32 || dtype == HICCL_FLOAT64 || dtype == HICCL_UINT64 ||
+      (dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_NATIVE)) {
     // Round 3, on the round-2 kernels (interleaved one-shot sweeps, n = 2 / 3 /
     // 4 / 8 x 32-144 MiB per input, f32 profiles/r03n_midsize.jsonl, bf16
-    // r03o_midsize_bf16.jsonl -- the same pattern; the C5 step shape scaled
-    // up, r03n_stepscale.jsonl): the phased engine needs both
+    // r03o_midsize_bf16.jsonl, f64 r03x_midsize_f64.jsonl -- the same
+    // pattern; u64 has f64's chunk and tile; the C5 step shape scaled up,
+    // r03n_stepscale.jsonl): the phased engine needs both
     // several chunks per CU and whole rounds of them -- one chunk per
     // workgroup (a CU per workgroup) is a single memory round trip with no
     // overlap, and a last round that only part of the grid works on (1.25 /

@@ -59,7 +59,7 @@ typedef enum {
  *          only); TILE with 32 KiB-per-input tiles (unroll 8) on the
  *          dynamic schedule with 2-4 inputs once every workgroup gets
  *          >= 128 of them (1 GiB per input, f32 / bf16); otherwise PHASE
- *          when its chunks fill the CUs -- f32 / bf16 native: >= 1 chunk per
+ *          when its chunks fill the CUs -- f32 / f64 / u64 / bf16 native: >= 1 chunk per
  *          CU with >= 5 inputs, >= 4 with 3-4, > 16 with 2, in rounds of
  *          chunks that keep >= 70 % / ~90 % / ~90 % of the CUs busy; other
  *          types: >= 1 chunk

@@ -166,10 +166,13 @@ def test_auto_choice_rule_table_on_host():
         ((f32, 16 * MiB // 4, 16), (T, 4, 4, 0)),   # 0.5 per CU: tiles, 4 workgroups per CU
         ((f32, 5 << 18, 2.4), (T, 2, 4, 0)),     # the C5 step's plan: half-size tiles
         ((bf16, 40 * MiB // 2, 3), (T, 4, 1, 0)),  # bf16 native: the f32 rule
+        ((L.HICCL_FLOAT64, 40 * MiB // 8, 3), (T, 4, 1, 0)),  # f64 / u64 too (r03x_midsize_f64.jsonl)
+        ((L.HICCL_FLOAT64, (1 << 26) // 2, 3), (P, 16, 1, 0)),
+        ((L.HICCL_UINT64, 40 * MiB // 8, 8), (T, 4, 1, 0)),
     ]
     for (dt, count, n), want in cases:
         assert _auto(dt, count, n) == want, (dt, count, n, _auto(dt, count, n), want)
-    # bf16 with the wide accumulator keeps the round-2 rule (PHASE from one chunk per CU)
+    # bf16 with the wide accumulator and int32 keep the round-2 rule (PHASE from one chunk per CU)
     assert _auto(bf16, 40 * MiB // 2, 3, acc=L.HICCL_ACC_WIDE)[0] == P
     # another CU count: the thresholds scale with it
     assert _auto(f32, 1 << 28, 8, cus=304)[0] == T
