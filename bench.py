@@ -1054,6 +1054,13 @@ def progstep(args):
         p_copy.launch([epoch[0]], err=err.data_ptr(), timeout_s=10.0, stream=stream)
         p_comp.launch([epoch[0]], err=err.data_ptr(), timeout_s=10.0, stream=stream)
 
+    def program_tail_folded_full():  # the prologue with release stores and fences (HICCL_PROG_FENCES=full)
+        os.environ["HICCL_PROG_FENCES"] = "full"
+        try:
+            program_tail_folded()
+        finally:
+            os.environ.pop("HICCL_PROG_FENCES", None)
+
     def separate_nophase():
         cp.enqueue(stream)
         comp.enqueue(stream)
@@ -1065,6 +1072,7 @@ def progstep(args):
         q_comp.launch(stream=stream)
 
     runs = {"separate": separate, "program": program, "program_tail_folded": program_tail_folded,
+            "program_tail_folded_full_fences": program_tail_folded_full,
             "separate_no_phases": separate_nophase, "program_no_phases": program_nophase}
     res = {k: [] for k in runs}
     for _ in range(5):
@@ -1084,8 +1092,10 @@ def progstep(args):
 
     side = torch.cuda.Stream()
     graphs = {}
-    for name in ("separate_graph", "program_tail_folded_graph", "separate_no_phases_graph",
-                 "program_no_phases_graph"):
+    for name in ("separate_graph", "program_tail_folded_graph", "program_tail_folded_full_fences_graph",
+                 "separate_no_phases_graph", "program_no_phases_graph"):
+        if name == "program_tail_folded_full_fences_graph":
+            os.environ["HICCL_PROG_FENCES"] = "full"  # read at each launch: the capture keeps it
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(side):
             cs = torch.cuda.current_stream()
@@ -1100,7 +1110,7 @@ def progstep(args):
                         phase_dev(f[1], e, s_)
                         comp.enqueue(cs)
                         phase_dev(f[2], e, s_)
-                    elif name == "program_tail_folded_graph":
+                    elif name in ("program_tail_folded_graph", "program_tail_folded_full_fences_graph"):
                         p_copy.launch([e], epoch_dev=ctr.data_ptr(), err=err.data_ptr(), timeout_s=10.0, stream=cs)
                         p_comp.launch([e], epoch_dev=ctr.data_ptr(), err=err.data_ptr(), timeout_s=10.0, stream=cs)
                     elif name == "separate_no_phases_graph":
@@ -1110,6 +1120,7 @@ def progstep(args):
                         q_copy.launch(stream=cs)
                         q_comp.launch(stream=cs)
         graphs[name] = g
+        os.environ.pop("HICCL_PROG_FENCES", None)
     for name, g in graphs.items():
         v = []
         for _ in range(5):

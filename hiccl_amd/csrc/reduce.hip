@@ -804,19 +804,36 @@ struct ProgArgs {
   const uint32_t *epoch_dev;
   uint64_t timeout_ticks;
   uint64_t nunits;
-  uint32_t stride, nphase, seq, pad;
+  uint32_t stride, nphase, seq;
+  uint32_t light;  // 1: relaxed token stores, no fences in the prologue (HICCL_PROG_FENCES, prog_light())
   uint32_t epoch[kProgMaxPhases];  // per launch: phase p stores / awaits epoch[p] (+ *epoch_dev)
 };
 
 // Phases [0, count) on one wave (lanes = flags), as k_sigwait_phases.
+//
+// `light` (the default, prog_light()): relaxed system-scope token stores
+// and no fence after the waits.  A program's tokens never publish data of
+// their own launch -- a done token follows the copies or reductions of an
+// EARLIER launch (complete, and released, at that kernel's end; a peer's
+// buffer written through with the peer policy), a ready token only says a
+// buffer an earlier launch read is free -- and this launch's units start
+// after the gate, on workgroups whose L1 holds none of their data (the
+// kernel-start acquire invalidated it and nothing read it since).  The wave
+// issues a phase's stores only after its polls of the previous phase have
+// returned (the loop exits on the loaded value).  Full mode (release stores,
+// an acquire-release fence per phase, a release gate store) is kept for A/B.
 __device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t count, uint32_t lane, uint32_t add) {
   for (uint32_t p = 0; p < count; p++) {
     const ConstU32 *q = (const ConstU32 *)&a.phase[p];
     const uint32_t s0 = q[0], s1 = q[1], w0 = q[2], w1 = q[3];
     const uint32_t epoch = a.epoch[p] + add;
-    for (uint32_t i = s0 + lane; i < s1; i += 64)
-      __hip_atomic_store(((uint32_t *const __attribute__((address_space(4))) *)a.sig)[i], epoch, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint32_t i = s0 + lane; i < s1; i += 64) {
+      uint32_t *f = ((uint32_t *const __attribute__((address_space(4))) *)a.sig)[i];
+      if (a.light)
+        __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else
+        __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     for (uint32_t i = w0 + lane; i < w1; i += 64) {
       const uint32_t *f = ((const uint32_t *const __attribute__((address_space(4))) *)a.wait)[i];
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -832,7 +849,7 @@ __device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t count, u
     }
     // every lane's waits of this phase precede any store of the next one
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+    if (!a.light) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
   }
 }
 
@@ -894,7 +911,12 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
     if (blockIdx.x == 0) {
       if (tid < 64) {
         prog_phases(a, a.nphase, (uint32_t)tid, add);
-        if (tid == 0) __hip_atomic_store(a.gate, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+          if (a.light)
+            __hip_atomic_store(a.gate, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            __hip_atomic_store(a.gate, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     } else if (tid == 0) {
       prog_gate_wait(a, seq);
@@ -2226,6 +2248,14 @@ prog_fn pick_prog(int dtype, int unroll) {
   }
 }
 
+// HICCL_PROG_FENCES=full: release token stores and a fence per phase (the
+// round-3 first version); default light (prog_phases).  Read at every launch
+// (a capture keeps the value it was recorded with).
+bool prog_light() {
+  const char *e = std::getenv("HICCL_PROG_FENCES");
+  return !(e && std::string(e) == "full");
+}
+
 void prog_quiesce(hiccl_program *p) {
   if (p->enqueued.load(std::memory_order_relaxed)) {
     (void)hipDeviceSynchronize();
@@ -2413,6 +2443,7 @@ int hiccl_program_launch(hiccl_program_t *p, const uint32_t *epochs, const uint3
   a.epoch_dev = epoch_dev;
   a.timeout_ticks = (uint64_t)((timeout_s > 0 ? timeout_s : 30.0) * 1e8);  // s_memrealtime: 100 MHz
   for (uint32_t i = 0; i < a.nphase; i++) a.epoch[i] = epochs[i];
+  a.light = prog_light() ? 1u : 0u;
   // the gate's sequence number: one per eager launch; a captured launch
   // uses seq + *epoch_dev (replay r: seq + r) and reserves 2^24 of them
   a.seq = ++p->seq;
