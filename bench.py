@@ -1054,6 +1054,13 @@ def progstep(args):
         p_copy.launch([epoch[0]], err=err.data_ptr(), timeout_s=10.0, stream=stream)
         p_comp.launch([epoch[0]], err=err.data_ptr(), timeout_s=10.0, stream=stream)
 
+    def separate_full():  # the signal kernels with release stores, acquire polls and fences
+        os.environ["HICCL_PROG_FENCES"] = "full"
+        try:
+            separate()
+        finally:
+            os.environ.pop("HICCL_PROG_FENCES", None)
+
     def program_tail_folded_full():  # the prologue with release stores and fences (HICCL_PROG_FENCES=full)
         os.environ["HICCL_PROG_FENCES"] = "full"
         try:
@@ -1071,7 +1078,8 @@ def progstep(args):
         q_copy.launch(stream=stream)
         q_comp.launch(stream=stream)
 
-    runs = {"separate": separate, "program": program, "program_tail_folded": program_tail_folded,
+    runs = {"separate": separate, "separate_full_fences": separate_full, "program": program,
+            "program_tail_folded": program_tail_folded,
             "program_tail_folded_full_fences": program_tail_folded_full,
             "separate_no_phases": separate_nophase, "program_no_phases": program_nophase}
     res = {k: [] for k in runs}

@@ -714,7 +714,8 @@ struct SigPhaseArgs {
   uint32_t *err;
   const uint32_t *epoch_dev;  // NULL, or a device word added to every epoch at run time (graph replays)
   uint64_t timeout_ticks;
-  uint32_t nphase, pad;
+  uint32_t nphase;
+  uint32_t light;  // 1: relaxed stores and polls, no fences (HICCL_PROG_FENCES, as the programs' prologue)
   uint32_t sig_end[kMaxPhases];   // phase p signals sig[sig_end[p-1] .. sig_end[p])
   uint32_t wait_end[kMaxPhases];  // and waits for wait[wait_end[p-1] .. wait_end[p])
   uint32_t epoch[kMaxPhases];
@@ -727,11 +728,20 @@ __global__ __launch_bounds__(64) void k_sigwait_phases(SigPhaseArgs a) {
   for (uint32_t p = 0; p < a.nphase; p++) {
     const uint32_t epoch = a.epoch[p] + add;
     const uint32_t s1 = a.sig_end[p], w1 = a.wait_end[p];
-    if (s0 + lane < s1) __hip_atomic_store(a.sig[s0 + lane], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (s0 + lane < s1) {
+      if (a.light)
+        __hip_atomic_store(a.sig[s0 + lane], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else
+        __hip_atomic_store(a.sig[s0 + lane], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (w0 + lane < w1) {
       const uint32_t *f = a.wait[w0 + lane];
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while ((int32_t)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      auto poll = [&]() {
+        return a.light ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                       : __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      };
+      while ((int32_t)(poll() - epoch) < 0) {
         __builtin_amdgcn_s_sleep(2);
         if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
@@ -742,7 +752,7 @@ __global__ __launch_bounds__(64) void k_sigwait_phases(SigPhaseArgs a) {
     }
     // every lane's waits of this phase precede any store of the next one
     __syncthreads();
-    __atomic_thread_fence(__ATOMIC_ACQ_REL);
+    if (!a.light) __atomic_thread_fence(__ATOMIC_ACQ_REL);
     s0 = s1;
     w0 = w1;
   }
@@ -937,6 +947,15 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
 }
 
 // ------------------------------------------------------------ host side ----
+
+// HICCL_PROG_FENCES=full: release token stores and fences in the token
+// phases of programs and of k_sigwait_phases (the round-3 first version);
+// default light (prog_phases).  Read at every launch
+// (a capture keeps the value it was recorded with).
+bool prog_light() {
+  const char *e = std::getenv("HICCL_PROG_FENCES");
+  return !(e && std::string(e) == "full");
+}
 
 struct DevInfo {
   int cus = 0;
@@ -2141,11 +2160,13 @@ int hiccl_signal_wait_phases(const hiccl_signal_phase_t *ph, int nph, const uint
   const uint64_t ticks = (uint64_t)((timeout_s > 0 ? timeout_s : 30.0) * 1e8);  // s_memrealtime: 100 MHz
   hipStream_t s = (hipStream_t)stream;
   SigPhaseArgs a;
+  const uint32_t light = prog_light() ? 1u : 0u;
   auto reset = [&]() {
     memset(&a, 0, sizeof(a));
     a.err = err;
     a.epoch_dev = epoch_dev;
     a.timeout_ticks = ticks;
+    a.light = light;
   };
   auto launch = [&]() -> int {
     if (!a.nphase) return 0;
@@ -2246,14 +2267,6 @@ prog_fn pick_prog(int dtype, int unroll) {
     case HICCL_BYTES: return u2 ? nullptr : launch_prog_t<OpRaw, 4>;
     default: return nullptr;
   }
-}
-
-// HICCL_PROG_FENCES=full: release token stores and a fence per phase (the
-// round-3 first version); default light (prog_phases).  Read at every launch
-// (a capture keeps the value it was recorded with).
-bool prog_light() {
-  const char *e = std::getenv("HICCL_PROG_FENCES");
-  return !(e && std::string(e) == "full");
 }
 
 void prog_quiesce(hiccl_program *p) {
