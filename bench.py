@@ -566,7 +566,7 @@ def main():
     ap.add_argument("--crossover", action="store_true")
     ap.add_argument("--planvs", action="store_true")
     ap.add_argument("--schedsweep", action="store_true")
-    ap.add_argument("--sweepdtype", default="f32", help="schedsweep: f32 | bf16 | f64 | u64")
+    ap.add_argument("--sweepdtype", default="f32", help="schedsweep: f32 | bf16 | bf16wide | f64 | u64 | i32")
     ap.add_argument("--sweepset", default="", help="schedsweep: '' (schedule/grab) | occupancy")
     ap.add_argument("--xdtype", default="both", help="crossover: f32 | bf16 | both")
     ap.add_argument("--xmib", default="", help="crossover: comma list of MiB per input")
@@ -891,13 +891,17 @@ def schedsweep(args):
                     ("phase_static", dict(engine=2, schedule=1)),
                     ("phase_dyn", dict(engine=2, schedule=2))]
     for n, mib in cases:
-        sdt = {"bf16": torch.bfloat16, "f64": torch.float64, "u64": torch.int64}.get(args.sweepdtype, torch.float32)
+        sdt = {"bf16": torch.bfloat16, "bf16wide": torch.bfloat16, "f64": torch.float64, "u64": torch.int64,
+               "i32": torch.int32}.get(args.sweepdtype, torch.float32)
+        wide = args.sweepdtype == "bf16wide"  # f32 accumulation (HICCL_ACC_WIDE) in every variant
         esz = torch.tensor([], dtype=sdt).element_size()
         count = (mib << 20) // esz
         ins, out = make_bucket(n, count, sdt)
         res = {}
         for rnd in range(5):
             for name, cfg in variants:
+                if wide:
+                    cfg = dict(cfg or {}, acc=1)
                 try:
                     _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins, config=cfg), max(args.steps, 10),
                                           args.warmup)
@@ -913,11 +917,17 @@ def schedsweep(args):
             t = float(np.median(v)) * 1e-3
             row[name] = round((n + 1) * count * esz / t / 1e9, 1)
         row["dtype"] = str(sdt).split(".")[-1]
-        if sdt in (torch.float64, torch.int64):  # the in-order sum on the device (f64 adds / u64 wrap-around)
+        if sdt in (torch.float64, torch.int64, torch.int32):  # in-order sum on the device (f64 adds, wrap-around ints)
             acc = torch.zeros_like(out)
             for t in ins:
                 acc = acc + t
-            row["parity_sample_ok"] = bool(torch.equal(acc.view(torch.int64), out.view(torch.int64)))
+            iv = torch.int32 if sdt == torch.int32 else torch.int64
+            row["parity_sample_ok"] = bool(torch.equal(acc.view(iv), out.view(iv)))
+        elif wide:  # one f32 accumulation, rounded once
+            acc = torch.zeros(out.shape, dtype=torch.float32, device=out.device)
+            for t in ins:
+                acc = acc + t.float()
+            row["parity_sample_ok"] = bool(torch.equal(acc.to(torch.bfloat16).view(torch.int16), out.view(torch.int16)))
         else:
             row["parity_sample_ok"] = sample_check(out, n, count, bf16=(sdt == torch.bfloat16))
         print(json.dumps(row), flush=True)
