@@ -1227,37 +1227,34 @@ int auto_engine(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
   const uint64_t chunk = (uint64_t)kPhBlock * phase_p_dtype(dtype, acc);
   const uint64_t cus = (uint64_t)device_cus(dev);
   const uint64_t per_cu = npkt / (cus * chunk);  // phased chunks per CU
-  if (dtype == HICCL_FLOAT32 || dtype == HICCL_FLOAT64 || dtype == HICCL_UINT64 ||
-      (dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_NATIVE)) {
-    // Round 3, on the round-2 kernels (interleaved one-shot sweeps, n = 2 / 3 /
-    // 4 / 8 x 32-144 MiB per input, f32 profiles/r03n_midsize.jsonl, bf16
-    // r03o_midsize_bf16.jsonl, f64 r03x_midsize_f64.jsonl -- the same
-    // pattern; u64 has f64's chunk and tile; the C5 step shape scaled up,
-    // r03n_stepscale.jsonl): the phased engine needs both
-    // several chunks per CU and whole rounds of them -- one chunk per
-    // workgroup (a CU per workgroup) is a single memory round trip with no
-    // overlap, and a last round that only part of the grid works on (1.25 /
-    // 1.5 / 2.5 chunks per CU) idles the rest: PHASE lost 3-20 % to static
-    // tiles there (n = 3 at 40 MiB: 5.08 vs 6.15 TB/s; the C5 step at 8 x
-    // 2^18: 29.6 vs 23.2 us).  `round_eff` = chunks / (whole rounds x CUs).
-    const uint64_t chunks = (npkt + chunk - 1) / chunk;
-    const double round_eff = chunks ? (double)chunks / (double)(((chunks + cus - 1) / cus) * cus) : 0.0;
-    if (n < 2.5) return per_cu > 16 && round_eff >= 0.89 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
-    if (n < kDynMinInputs) return per_cu >= 4 && round_eff >= 0.89 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
-    // many inputs, under the dynamic tiles' ticket count: PHASE from one
-    // whole chunk per CU unless a third of the last round idles (n = 8 at
-    // 40 MiB: tiles 6.03 vs 5.45; at 48 / 80 MiB PHASE holds: 6.08 / 6.25);
-    // from 16 inputs a chunk is >= 2 MiB of reads, and PHASE leads already
-    // with 70 % of the CUs holding one (24 MiB per input, 0.75 chunks per CU:
-    // n = 16 / 32 PHASE 6.56 / 6.34 vs tiles 6.15-6.25; at 0.5 per CU tiles
-    // lead: 6.21 / 6.25 vs 5.43 / 5.61; profiles/r03q_sweep_manyn.jsonl)
-    return (per_cu >= 1 || n >= 16) && round_eff >= 0.7 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
-  }
-  // two inputs: the static tile order leads from 2 to 16 chunks per CU (f32
-  // 64-512 MiB per input: +1-4 %), the phased order below and above it
-  // (32 MiB: 5.49 vs 5.17; 1 GiB: 6.13 vs 5.96 TB/s; r01g_xover_smalln.jsonl)
-  if (n < 2.5 && per_cu >= 2 && per_cu <= 16) return HICCL_ENGINE_TILE;
-  return per_cu >= kPhaseMinChunksPerCU ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
+  // Round 3, on the round-2 kernels (interleaved one-shot sweeps of n = 2 /
+  // 3 / 4 / 8 at 1-4.5 chunks per CU: f32 profiles/r03n_midsize.jsonl, bf16
+  // r03o_midsize_bf16.jsonl, f64 r03x_midsize_f64.jsonl, int32 and bf16 with
+  // the f32 accumulator -- 64 KiB chunks -- r03ze_midsize_i32.jsonl /
+  // r03ze_midsize_bf16wide.jsonl; the C5 step shape scaled up,
+  // r03n_stepscale.jsonl): the phased engine needs both several chunks per
+  // CU and whole rounds of them -- one chunk per workgroup (a CU per
+  // workgroup) is a single memory round trip with no overlap, and a last
+  // round that only part of the grid works on (1.25 / 1.5 / 2.5 chunks per
+  // CU) idles the rest: PHASE lost 3-20 % to static tiles there (f32 n = 3
+  // at 40 MiB: 5.08 vs 6.15 TB/s; the C5 step at 8 x 2^18: 29.6 vs 23.2
+  // us).  `round_eff` = chunks / (whole rounds x CUs).
+  const bool big_chunk = chunk >= 8192;  // 128 KiB per input (P = 16)
+  const uint64_t chunks = (npkt + chunk - 1) / chunk;
+  const double round_eff = chunks ? (double)chunks / (double)(((chunks + cus - 1) / cus) * cus) : 0.0;
+  if (n < 2.5) return per_cu > 16 && round_eff >= 0.89 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
+  if (n < kDynMinInputs) return per_cu >= 4 && round_eff >= 0.89 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
+  // many inputs, under the dynamic tiles' ticket count: PHASE from one
+  // whole chunk per CU unless too much of the last round idles (f32 n = 8 at
+  // 40 MiB, 1.25 per CU: tiles 6.03 vs 5.45; at 48 / 80 MiB PHASE holds:
+  // 6.08 / 6.25; with 64 KiB chunks PHASE needs 80 %: int32 / bf16-wide n =
+  // 8 at 1.5 per CU: tiles 5.84 / 5.94 vs 5.58 / 5.68); from 16 inputs a
+  // 128 KiB chunk is >= 2 MiB of reads, and PHASE leads already with 70 %
+  // of the CUs holding one (24 MiB per input, 0.75 chunks per CU: n = 16 /
+  // 32 PHASE 6.56 / 6.34 vs tiles 6.15-6.25; at 0.5 per CU tiles lead:
+  // 6.21 / 6.25 vs 5.43 / 5.61; profiles/r03q_sweep_manyn.jsonl)
+  const bool enough = per_cu >= 1 || (n >= 16 && big_chunk);
+  return enough && round_eff >= (big_chunk ? 0.7 : 0.8) ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
 }
 
 // Workgroups per CU: a tile launch too small for a phased chunk per CU has

@@ -59,11 +59,10 @@ typedef enum {
  *          only); TILE with 32 KiB-per-input tiles (unroll 8) on the
  *          dynamic schedule with 2-4 inputs once every workgroup gets
  *          >= 128 of them (1 GiB per input, f32 / bf16); otherwise PHASE
- *          when its chunks fill the CUs -- f32 / f64 / u64 / bf16 native: >= 1 chunk per
- *          CU with >= 5 inputs, >= 4 with 3-4, > 16 with 2, in rounds of
- *          chunks that keep >= 70 % / ~90 % / ~90 % of the CUs busy; other
- *          types: >= 1 chunk
- *          per CU (two inputs: not at 2-16 chunks per CU) -- else TILE,
+ *          when its chunks fill the CUs: >= 1 chunk per CU with >= 5
+ *          inputs (with >= 16 inputs and 128 KiB chunks 0.7 suffice), >= 4
+ *          with 3-4, > 16 with 2, in rounds of chunks that keep >= 70 % (64
+ *          KiB chunks: 80 %) / ~90 % / ~90 % of the CUs busy -- else TILE,
  *          with 4 workgroups per CU below one chunk per CU (unroll 2 below
  *          two 16 KiB tiles per CU) (one-shot: that call; plan: all
  *          computes, packet-weighted mean n). */

@@ -172,8 +172,13 @@ def test_auto_choice_rule_table_on_host():
     ]
     for (dt, count, n), want in cases:
         assert _auto(dt, count, n) == want, (dt, count, n, _auto(dt, count, n), want)
-    # bf16 with the wide accumulator and int32 keep the round-2 rule (PHASE from one chunk per CU)
-    assert _auto(bf16, 40 * MiB // 2, 3, acc=L.HICCL_ACC_WIDE)[0] == P
+    # 64 KiB phased chunks (bf16 with the f32 accumulator, int32): the same rule
+    # in chunks, PHASE for many inputs only when 80 % of the last round is busy
+    # (profiles/r03ze_midsize_i32.jsonl, r03ze_midsize_bf16wide.jsonl)
+    assert _auto(bf16, 40 * MiB // 2, 3, acc=L.HICCL_ACC_WIDE)[0] == T   # 2.5 chunks per CU
+    assert _auto(bf16, 72 * MiB // 2, 4, acc=L.HICCL_ACC_WIDE)[0] == P   # 4.5, 90 % busy
+    assert _auto(L.HICCL_INT32, 24 * MiB // 4, 8)[0] == T                # 1.5, 75 % busy
+    assert _auto(L.HICCL_INT32, 40 * MiB // 4, 8)[0] == P                # 2.5, 83 % busy
     # another CU count: the thresholds scale with it
     assert _auto(f32, 1 << 28, 8, cus=304)[0] == T
     lib = L.lib()
