@@ -264,3 +264,20 @@ def test_fused_gather_plan(cfg):
     for rank in range(np_):
         a, b = fmem[(rank, ("recv",))], omem[(rank, ("recv",))]
         assert a.tobytes() == b.tobytes(), f"rank {rank}: {int((a != b).sum())} elements differ"
+
+
+def test_consecutive_steps_share_buffers():
+    """DESIGN.md section 8 (Next 3): under the reference's buffer recycling a
+    pipeline step's copies write the receive buffers the previous step's
+    reductions read, so the two cannot share a launch -- tools/step_overlap.py
+    over every rank of the C++ factorization (the {1,4,2} all-reduce at
+    pipedepth 4 and 16, a flat {8})."""
+    if not os.path.exists(DUMP):
+        subprocess.run(["make", "-C", ROOT, "build/plan_dump"], check=True, stdout=subprocess.DEVNULL)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import step_overlap
+    for args, most in ((["8", "8", "4096", "1", "1", "4", "1,4,2", "mpi,ipc,ipc"], 1),
+                       (["8", "8", "65536", "1", "1", "16", "1,4,2", "mpi,ipc,ipc"], 1),
+                       (["8", "8", "65536", "1", "1", "16", "8", "ipc"], 0)):
+        for r in step_overlap.analyze(args):
+            assert r["pairs"] > 0 and r["independent_pairs"] <= most, (args, r)
