@@ -282,11 +282,15 @@ void hiccl_host_pipe_destroy(hiccl_host_pipe_t *pipe);
 /* ----------------------------------------------------------------------
  * Stream-ordered signalling for the transport (include/hiccl/transport.h).
  *
- * Enqueues on `stream` (after all earlier work on it): a system-scope
- * release store of `epoch` to each of the nsig flags `sig` (typically flags
- * in a peer's IPC-mapped device memory), then a bounded spin until each of
- * the nwait local flags `wait` holds a value >= epoch (32-bit wrap-aware),
- * with system-scope acquire.  A spin exceeding timeout_s (<= 0: 30 s) stores
+ * Enqueues on `stream` (after all earlier work on it): a system-scope store
+ * of `epoch` to each of the nsig flags `sig` (typically flags in a peer's
+ * IPC-mapped device memory), then a bounded spin until each of the nwait
+ * local flags `wait` holds a value >= epoch (32-bit wrap-aware).  The
+ * stores and polls are relaxed (HICCL_PROG_FENCES=full: release stores,
+ * acquire polls): a token orders launches and publishes nothing of its own
+ * launch, so data it announces must be complete when the launch that wrote
+ * it ended -- written through to a peer's memory with
+ * hiccl_reduce_plan_set_peer.  A spin exceeding timeout_s (<= 0: 30 s) stores
  * 1 to *err (if err is not NULL; host-visible memory recommended) and gives
  * up instead of hanging.  Replaces, per pipeline step, the host round trip
  * the reference's transport makes around every transfer (comm.h:188-204).
@@ -331,7 +335,8 @@ int hiccl_signal_wait_phases(const hiccl_signal_phase_t *phases, int nphases, co
  * computes -- plans' computes, reductions of the program's dtype or
  * HICCL_BYTES exact copies, all independent of each other -- which start
  * only after the last phase.  Same stores, waits and results as the
- * separate launches, one kernel boundary fewer per phase group.
+ * separate launches (the same relaxed tokens), one kernel boundary fewer
+ * per phase group.
  *
  * add_signal appends one phase (only before the first add_plan); its epoch
  *   is supplied per launch.
