@@ -4,6 +4,7 @@ The oracle (oracle/liboracle.so) is test infrastructure only: it is loaded
 here as the checker, never by the product package.
 """
 import ctypes
+import fcntl
 import json
 import os
 import subprocess
@@ -27,10 +28,19 @@ def pytest_collection_modifyitems(config, items):
     items.sort(key=lambda it: it.get_closest_marker("runtime_probe") is not None)  # stable: order kept otherwise
 
 
+def make(directory, *targets):
+    """`make -C directory targets` under a lock file, so that test workers
+    (pytest -n) never run make on the same targets at once (a header edited
+    since the last build sends every worker into the same rebuild)."""
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".make.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", directory, *targets], check=True, stdout=subprocess.DEVNULL)
+
+
 def _build_oracle():
     if not os.path.exists(ORACLE_SO):
-        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "liboracle.so"], check=True,
-                       stdout=subprocess.DEVNULL)
+        make(os.path.join(ROOT, "oracle"), "liboracle.so")
 
 
 class Oracle:

@@ -12,6 +12,7 @@ import sys
 
 import pytest
 import torch.multiprocessing as mp
+from conftest import make
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -169,7 +170,7 @@ def test_c5_driver_json_records_devices_and_mode(tmp_path):
     mpirun = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
     if not os.path.exists(mpirun):
         pytest.skip("no mpirun")
-    subprocess.run(["make", "-C", ROOT, "build/collectives_host_f32"], check=True, stdout=subprocess.DEVNULL)
+    make(ROOT, "build/collectives_host_f32")
     path = tmp_path / "c5.json"
     env = dict(os.environ, OMP_NUM_THREADS="1", HICCL_DRIVER_JSON=str(path))
     p = subprocess.run([mpirun, "-np", "2", os.path.join(ROOT, "build", "collectives_host_f32"), "8", "4096", "1", "1",

@@ -21,6 +21,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import schedule as S  # noqa: E402
+from conftest import make
 
 MPIRUN = shutil.which("mpirun") or "/opt/conda/bin/mpirun"
 HOST = os.path.join(ROOT, "build", "collectives_host")
@@ -31,8 +32,7 @@ pytestmark = pytest.mark.skipif(not os.path.exists(MPIRUN), reason="no mpirun")
 
 @pytest.fixture(scope="module", autouse=True)
 def built():
-    subprocess.run(["make", "-C", ROOT, "build/collectives_host", "build/collectives_host_f32",
-                    "build/readme_example_host"], check=True, stdout=subprocess.DEVNULL)
+    make(ROOT, "build/collectives_host", "build/collectives_host_f32", "build/readme_example_host")
 
 
 def mpirun(np_, exe, args, timeout=240):

@@ -21,6 +21,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import schedule as S  # noqa: E402
+from conftest import make
 
 DUMP = os.path.join(ROOT, "build", "plan_dump")
 LIBS = {"mpi": S.MPI, "ipc": S.IPC, "ipc_get": S.IPC_GET, "xccl": S.XCCL}
@@ -29,7 +30,7 @@ SEND, RECV, TMP = 1 << 40, 2 << 40, 3 << 40
 
 @pytest.fixture(scope="module", autouse=True)
 def built():
-    subprocess.run(["make", "-C", ROOT, "build/plan_dump"], check=True, stdout=subprocess.DEVNULL)
+    make(ROOT, "build/plan_dump")
 
 
 def inputs(np_, n):
@@ -273,7 +274,7 @@ def test_consecutive_steps_share_buffers():
     over every rank of the C++ factorization (the {1,4,2} all-reduce at
     pipedepth 4 and 16, a flat {8})."""
     if not os.path.exists(DUMP):
-        subprocess.run(["make", "-C", ROOT, "build/plan_dump"], check=True, stdout=subprocess.DEVNULL)
+        make(ROOT, "build/plan_dump")
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import step_overlap
     for args, most in ((["8", "8", "4096", "1", "1", "4", "1,4,2", "mpi,ipc,ipc"], 1),
