@@ -37,6 +37,31 @@ grep -q 'void reduce_kernel' <<<"$FRAG" || { echo "build_ref: reduce_kernel not 
 } | g++ -x c++ -std=c++17 -O3 -fopenmp -fPIC -shared -o "$OUT" -
 echo "build_ref: built $OUT from $SRC"
 
+# The same fragment instantiated for bf16 with ROCm's own host bf16 type,
+# __hip_bfloat16 (<hip/hip_bf16.h>: `T acc = 0` and `acc += x` are the
+# compiler's __bf16 add, rounded to bf16 after every add) -- the type a HIP
+# user of reduce_kernel<T> would instantiate.  clang++ (ROCm's) is needed for
+# __bf16 on the host; no OpenMP runtime is linked (the pragma is ignored, the
+# loop's result does not depend on it).
+OUT16="$(dirname "$OUT")/libhiccl_ref_bf16.so"
+CLANG=/opt/rocm/llvm/bin/clang++
+if [ -x "$CLANG" ] && [ -f /opt/rocm/include/hip/hip_bf16.h ]; then
+  {
+    echo '#include <cstddef>'
+    echo '#include <cstdint>'
+    echo '#include <hip/hip_bf16.h>'
+    echo 'namespace HiCCL {'
+    echo "#line 14 \"$SRC\""
+    echo "$FRAG"
+    echo '}'
+    echo '#line 1 "oracle/build_ref.sh:wrapper_bf16"'
+    echo 'static_assert(sizeof(__hip_bfloat16) == 2, "bf16 storage");'
+    echo 'extern "C" void ref_reduce_bf16(uint16_t *o, size_t c, uint16_t **in, int n) {'
+    echo '  HiCCL::reduce_kernel<__hip_bfloat16>(reinterpret_cast<__hip_bfloat16 *>(o), c, reinterpret_cast<__hip_bfloat16 **>(in), n); }'
+  } | "$CLANG" -x c++ -std=c++17 -O2 -Wno-unknown-pragmas -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -fPIC -shared -o "$OUT16" -
+  echo "build_ref: built $OUT16 from $SRC (reduce_kernel<__hip_bfloat16>)"
+fi
+
 # ---------------------------------------------------------------------------
 # Drop-in check: the reference's OWN driver, collectives/main.cpp, compiled
 # unmodified against THIS build's include/hiccl.h.  The source is fed on

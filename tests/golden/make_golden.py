@@ -11,9 +11,11 @@ Expected outputs come from the REFERENCE ITSELF: HiCCL's CPU
 ``reduce_kernel<T>`` (source/compute.h:14-23), compiled unmodified from the
 reference tree by oracle/build_ref.sh into oracle/_ref/libhiccl_ref.so.  The
 CPU restatement (oracle/liboracle.so) is run on every case too and must agree
-bit for bit -- this is what pins the oracle.  bf16 is not instantiable in the
-reference (its drivers use size_t / float), so bf16 fixtures come from the
-oracle only and are marked ``pinned_by = "oracle"``.
+bit for bit -- this is what pins the oracle.  The reference's drivers use
+size_t / float; for bf16 the same reduce_kernel<T> is instantiated with ROCm's
+own host bf16 type, __hip_bfloat16 (oracle/_ref/libhiccl_ref_bf16.so, see
+oracle/build_ref.sh), and must agree with the restatement bit for bit (NaN
+outputs: NaN-ness only -- the payload of a NaN is not part of the contract).
 
 Each fixture file is an .npz of plain numeric arrays (no pickles):
   <case>/in   (n, count) inputs in summation order
@@ -39,8 +41,13 @@ NS = [1, 2, 3, 4, 7, 8, 64]
 
 def load_libs():
     ref = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libhiccl_ref.so"))
+    ref16 = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libhiccl_ref_bf16.so"))
     ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
-    return ref, ora
+    return ref, ref16, ora
+
+
+def bf16_nan(a):
+    return ((a & 0x7F80) == 0x7F80) & ((a & 0x7F) != 0)
 
 
 def ptr_table(arrs):
@@ -127,20 +134,23 @@ def sha(path):
 
 
 def main():
-    ref, ora = load_libs()
+    ref, ref16, ora = load_libs()
     rng = np.random.default_rng(SEED)
     manifest = {"seed": SEED, "generator": "tests/golden/make_golden.py",
-                "reference": "source/compute.h:14-23 reduce_kernel<T> (oracle/_ref/libhiccl_ref.so)",
+                "reference": "source/compute.h:14-23 reduce_kernel<T> (oracle/_ref/libhiccl_ref.so; bf16: "
+                             "reduce_kernel<__hip_bfloat16>, oracle/_ref/libhiccl_ref_bf16.so)",
                 "files": {}}
 
     def check(name, dtype, ref_fn, ora_fn, inputs, count):
-        exp = run(ref, ref_fn, dtype, inputs, count) if ref_fn else None
+        exp = run(ref16 if ref_fn == "ref_reduce_bf16" else ref, ref_fn, dtype, inputs, count)
         got = run(ora, ora_fn, dtype, inputs, count)
-        if exp is not None:
-            if exp.tobytes() != got.tobytes():
+        if ref_fn == "ref_reduce_bf16":
+            na, ng = bf16_nan(exp), bf16_nan(got)
+            if not (np.array_equal(na, ng) and np.array_equal(exp[~na], got[~ng])):
                 raise SystemExit(f"oracle disagrees with the reference on {name}")
-            return exp
-        return got
+        elif exp.tobytes() != got.tobytes():
+            raise SystemExit(f"oracle disagrees with the reference on {name}")
+        return exp
 
     # ---- f32
     cases = {}
@@ -185,16 +195,18 @@ def main():
     cases["wrap_n4"] = (x, check("u64wrap", np.uint64, "ref_reduce_u64", "oracle_reduce_u64", list(x), 1031))
     save("reduce_u64", cases, manifest, "reference")
 
-    # ---- bf16 (oracle-pinned: the reference never instantiates bf16)
+    # ---- bf16: reduce_kernel<__hip_bfloat16>
     cases = {}
     for n in (1, 2, 3, 8, 16):
         for c in (1, 7, 8, 9, 257, 4099):
             xf = fill_uniform(ora, n, c)
             x = f32_to_bf16_bits(xf * np.float32(n))  # spread magnitudes a little
-            cases[f"rand_n{n}_c{c}"] = (x, check("bf16", np.uint16, None, "oracle_reduce_bf16", list(x), c))
+            cases[f"rand_n{n}_c{c}"] = (x, check("bf16", np.uint16, "ref_reduce_bf16", "oracle_reduce_bf16",
+                                                  list(x), c))
     sp = f32_to_bf16_bits(special_f32())
-    cases["special_n3"] = (sp, check("bf16sp", np.uint16, None, "oracle_reduce_bf16", list(sp), sp.shape[1]))
-    save("reduce_bf16", cases, manifest, "oracle")
+    cases["special_n3"] = (sp, check("bf16sp", np.uint16, "ref_reduce_bf16", "oracle_reduce_bf16", list(sp),
+                                        sp.shape[1]))
+    save("reduce_bf16", cases, manifest, "reference")
 
     with open(os.path.join(HERE, "manifest.json"), "w") as fh:
         json.dump(manifest, fh, indent=1, sort_keys=True)

@@ -5,7 +5,9 @@
   reproduces every committed fixture bit for bit -- the f32 / f64 / size_t
   fixtures were produced by the REFERENCE's own reduce_kernel compiled from
   /root/reference (tests/golden/make_golden.py);
-* where the compiled reference is present (build container), it is re-run;
+* where the compiled reference is present (build container), it is re-run
+  (bf16: reduce_kernel<__hip_bfloat16>, on the fixtures and on inputs drawn
+  from every bf16 bit pattern);
 * an independent numpy restatement (sequential adds in list order) agrees;
 * the synthetic-input generator matches a numpy restatement of the hash.
 """
@@ -28,6 +30,7 @@ def test_manifest_hashes(manifest):
             assert hashlib.sha256(fh.read()).hexdigest() == meta["sha256"], fname
     assert manifest["files"]["reduce_f32.npz"]["pinned_by"] == "reference"
     assert manifest["files"]["reduce_u64.npz"]["pinned_by"] == "reference"
+    assert manifest["files"]["reduce_bf16.npz"]["pinned_by"] == "reference"
 
 
 @pytest.mark.parametrize("name", sorted(DTYPES))
@@ -52,6 +55,46 @@ def test_reference_rerun_matches_golden():
         tab = (ctypes.c_void_p * max(1, len(rows)))(*[r.ctypes.data for r in rows])
         f(ctypes.c_void_p(out.ctypes.data), ctypes.c_size_t(len(y)), tab, ctypes.c_int(len(rows)))
         assert out.tobytes() == y.tobytes(), case
+
+
+REF16_SO = os.path.join(os.path.dirname(REF_SO), "libhiccl_ref_bf16.so")
+
+
+def _ref16():
+    f = ctypes.CDLL(REF16_SO).ref_reduce_bf16
+    f.restype = None
+
+    def run(x, count):
+        out = np.full(count, 0x7F7F, np.uint16)
+        rows = [np.ascontiguousarray(r) for r in x]
+        tab = (ctypes.c_void_p * max(1, len(rows)))(*[r.ctypes.data for r in rows])
+        f(ctypes.c_void_p(out.ctypes.data), ctypes.c_size_t(count), tab, ctypes.c_int(len(rows)))
+        return out
+    return run
+
+
+@pytest.mark.skipif(not os.path.exists(REF16_SO), reason="compiled reference only in the build container")
+def test_reference_bf16_rerun_matches_golden():
+    """reduce_kernel<__hip_bfloat16> (compute.h:14-23 with ROCm's host bf16
+    type, oracle/build_ref.sh) reproduces every bf16 fixture bit for bit."""
+    run = _ref16()
+    for case, d in load_golden("reduce_bf16").items():
+        assert run(d["in"], len(d["out"])).tobytes() == d["out"].tobytes(), case
+
+
+@pytest.mark.skipif(not os.path.exists(REF16_SO), reason="compiled reference only in the build container")
+def test_oracle_bf16_vs_reference_every_bit_pattern(oracle):
+    """Inputs drawn from all 65,536 bf16 bit patterns (NaN, Inf, denormals,
+    signed zeros), 0-19 inputs: the restatement equals reduce_kernel<
+    __hip_bfloat16> on every element (a NaN output's payload aside)."""
+    run = _ref16()
+    rng = np.random.default_rng(5)
+    for _ in range(60):
+        n, c = int(rng.integers(0, 20)), int(rng.integers(1, 3000))
+        x = rng.integers(0, 1 << 16, size=(n, c), dtype=np.uint32).astype(np.uint16)
+        want = run(list(x), c)
+        got = oracle.reduce(list(x), count=c, dtype=np.uint16)
+        assert bits_equal(got, want), (n, c, first_mismatch(got, want))
 
 
 def _numpy_sequential(x, dtype):
