@@ -12,7 +12,7 @@
 # .gitmodules:1-3) is NOT built.  It is wrapped in `namespace HiCCL` exactly
 # as hiccl.h:29,43 includes it, and explicitly instantiated for the types the
 # reference drivers use (float: main.cu:10; size_t: collectives/main.cpp:24)
-# plus double.
+# plus double and int32.
 #
 # usage: build_ref.sh <reference-root> <output.so>
 set -euo pipefail
@@ -34,7 +34,10 @@ grep -q 'void reduce_kernel' <<<"$FRAG" || { echo "build_ref: reduce_kernel not 
   echo 'extern "C" void ref_reduce_f32(float *o, size_t c, float **in, int n) { HiCCL::reduce_kernel<float>(o, c, in, n); }'
   echo 'extern "C" void ref_reduce_f64(double *o, size_t c, double **in, int n) { HiCCL::reduce_kernel<double>(o, c, in, n); }'
   echo 'extern "C" void ref_reduce_u64(size_t *o, size_t c, size_t **in, int n) { HiCCL::reduce_kernel<size_t>(o, c, in, n); }'
-} | g++ -x c++ -std=c++17 -O3 -fopenmp -fPIC -shared -o "$OUT" -
+  echo 'extern "C" void ref_reduce_i32(int32_t *o, size_t c, int32_t **in, int n) { HiCCL::reduce_kernel<int32_t>(o, c, in, n); }'
+} | g++ -x c++ -std=c++17 -O3 -fopenmp -fwrapv -fPIC -shared -o "$OUT" -
+# (-fwrapv: a signed int32 sum that overflows wraps in two's complement, as
+# the GPU's integer adds do, instead of being undefined in C++)
 echo "build_ref: built $OUT from $SRC"
 
 # The same fragment instantiated for bf16 with ROCm's own host bf16 type,

@@ -195,6 +195,15 @@ def main():
     cases["wrap_n4"] = (x, check("u64wrap", np.uint64, "ref_reduce_u64", "oracle_reduce_u64", list(x), 1031))
     save("reduce_u64", cases, manifest, "reference")
 
+    # ---- int32: small values, and full-range values whose sums wrap
+    cases = {}
+    for n in (1, 2, 3, 8):
+        x = rng.integers(-1000, 1000, size=(n, 4099), dtype=np.int64).astype(np.int32)
+        cases[f"small_n{n}"] = (x, check("i32", np.int32, "ref_reduce_i32", "oracle_reduce_i32", list(x), 4099))
+    x = rng.integers(-2**31, 2**31, size=(5, 1031), dtype=np.int64).astype(np.int32)
+    cases["wrap_n5"] = (x, check("i32wrap", np.int32, "ref_reduce_i32", "oracle_reduce_i32", list(x), 1031))
+    save("reduce_i32", cases, manifest, "reference")
+
     # ---- bf16: reduce_kernel<__hip_bfloat16>
     cases = {}
     for n in (1, 2, 3, 8, 16):

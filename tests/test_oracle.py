@@ -21,7 +21,7 @@ import pytest
 from conftest import GOLDEN, REF_SO, bits_equal, first_mismatch, load_golden
 
 DTYPES = {"reduce_f32": np.float32, "reduce_f64": np.float64, "reduce_u64": np.uint64,
-          "reduce_bf16": np.uint16}
+          "reduce_bf16": np.uint16, "reduce_i32": np.int32}
 
 
 def test_manifest_hashes(manifest):
@@ -31,6 +31,7 @@ def test_manifest_hashes(manifest):
     assert manifest["files"]["reduce_f32.npz"]["pinned_by"] == "reference"
     assert manifest["files"]["reduce_u64.npz"]["pinned_by"] == "reference"
     assert manifest["files"]["reduce_bf16.npz"]["pinned_by"] == "reference"
+    assert manifest["files"]["reduce_i32.npz"]["pinned_by"] == "reference"
 
 
 @pytest.mark.parametrize("name", sorted(DTYPES))
@@ -44,11 +45,13 @@ def test_oracle_matches_golden(oracle, name):
 
 
 @pytest.mark.skipif(not os.path.exists(REF_SO), reason="compiled reference only in the build container")
-def test_reference_rerun_matches_golden():
+@pytest.mark.parametrize("name,fn", [("reduce_f32", "ref_reduce_f32"), ("reduce_f64", "ref_reduce_f64"),
+                                     ("reduce_u64", "ref_reduce_u64"), ("reduce_i32", "ref_reduce_i32")])
+def test_reference_rerun_matches_golden(name, fn):
     ref = ctypes.CDLL(REF_SO)
-    f = ref.ref_reduce_f32
+    f = getattr(ref, fn)
     f.restype = None
-    for case, d in load_golden("reduce_f32").items():
+    for case, d in load_golden(name).items():
         x, y = d["in"], d["out"]
         out = np.empty_like(y)
         rows = [np.ascontiguousarray(r) for r in x]

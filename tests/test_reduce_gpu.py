@@ -23,7 +23,7 @@ DEV = "cuda:0"
 PHASE = dict(engine=hiccl_amd.HICCL_ENGINE_PHASE)
 ENGINES = pytest.mark.parametrize("eng", [None, PHASE], ids=["auto", "phase"])
 TORCH_OF = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
-            np.dtype(np.uint64): torch.int64, np.dtype(np.uint16): torch.bfloat16}
+            np.dtype(np.uint64): torch.int64, np.dtype(np.uint16): torch.bfloat16, np.dtype(np.int32): torch.int32}
 
 
 def to_dev(a):
@@ -71,7 +71,8 @@ def gpu_reduce(x, count, dtype, offsets=None, out_offset=0, config=None):
 
 
 @pytest.mark.parametrize("name,dtype", [("reduce_f32", np.float32), ("reduce_f64", np.float64),
-                                        ("reduce_u64", np.uint64), ("reduce_bf16", np.uint16)])
+                                        ("reduce_u64", np.uint64), ("reduce_bf16", np.uint16),
+                                        ("reduce_i32", np.int32)])
 @ENGINES
 def test_golden_fixtures(name, dtype, eng):
     for case, d in load_golden(name).items():
