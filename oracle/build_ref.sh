@@ -66,6 +66,44 @@ if [ -x "$CLANG" ] && [ -f /opt/rocm/include/hip/hip_bf16.h ]; then
 fi
 
 # ---------------------------------------------------------------------------
+# The reference's own GPU kernel (compute.h:2-12, the PORT_CUDA / PORT_HIP
+# branch: the lines between `#if defined PORT_CUDA || defined PORT_HIP` and
+# the first `#else`), compiled for gfx950 by hipcc into
+# oracle/_ref/libhiccl_ref_hip.so, with launchers that launch it exactly as
+# Compute<T>::start does (compute.h:88-91: block 256, ceil(count / 256)
+# workgroups, the caller's stream, a device array of input pointers).  The
+# GPU tier compares this build's kernels with it on the same device (bits and
+# time, tests/test_ref_hip_gpu.py); nothing in the product calls it.
+OUTHIP="$(dirname "$OUT")/libhiccl_ref_hip.so"
+GFRAG=$(awk '/^#if defined PORT_CUDA \|\| defined PORT_HIP/{f=1;next} /^#else/{if(f)exit} f' "$SRC")
+if [ -x /opt/rocm/bin/hipcc ] && grep -q '__global__ void reduce_kernel' <<<"$GFRAG"; then
+  TMPD=$(mktemp -d)
+  {
+    echo '#include <hip/hip_runtime.h>'
+    echo '#include <hip/hip_bf16.h>'
+    echo '#include <cstddef>'
+    echo '#include <cstdint>'
+    echo 'namespace HiCCL {'
+    echo "#line 3 \"$SRC\""
+    echo "$GFRAG"
+    echo '}'
+    echo '#line 1 "oracle/build_ref.sh:wrapper_hip"'
+    echo 'template <typename T> static int launch(T *o, size_t c, T **in_d, int n, hipStream_t s) {'
+    echo '  int blocksize = 256;'
+    echo '  if (c) HiCCL::reduce_kernel<T><<<(c + blocksize - 1) / blocksize, blocksize, 0, s>>>(o, c, in_d, n);'
+    echo '  return (int)hipGetLastError(); }'
+    echo 'extern "C" int ref_hip_reduce_f32(float *o, size_t c, float **in_d, int n, hipStream_t s) { return launch(o, c, in_d, n, s); }'
+    echo 'extern "C" int ref_hip_reduce_f64(double *o, size_t c, double **in_d, int n, hipStream_t s) { return launch(o, c, in_d, n, s); }'
+    echo 'extern "C" int ref_hip_reduce_u64(size_t *o, size_t c, size_t **in_d, int n, hipStream_t s) { return launch(o, c, in_d, n, s); }'
+    echo 'extern "C" int ref_hip_reduce_i32(int32_t *o, size_t c, int32_t **in_d, int n, hipStream_t s) { return launch(o, c, in_d, n, s); }'
+    echo 'extern "C" int ref_hip_reduce_bf16(__hip_bfloat16 *o, size_t c, __hip_bfloat16 **in_d, int n, hipStream_t s) { return launch(o, c, in_d, n, s); }'
+  } > "$TMPD/ref_gpu.hip"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -o "$OUTHIP" "$TMPD/ref_gpu.hip"
+  rm -rf "$TMPD"
+  echo "build_ref: built $OUTHIP from $SRC (reduce_kernel<T> GPU branch, gfx950)"
+fi
+
+# ---------------------------------------------------------------------------
 # Drop-in check: the reference's OWN driver, collectives/main.cpp, compiled
 # unmodified against THIS build's include/hiccl.h.  The source is fed on
 # stdin from inside include/hiccl/, so its `#include "../hiccl.h"`

@@ -1,0 +1,261 @@
+"""GPU tier: this build against the reference's OWN GPU kernel on the same MI355X.
+
+`reduce_kernel<T>` (/root/reference/source/compute.h:2-12, the PORT_HIP
+branch) is compiled for gfx950 from the reference tree by oracle/build_ref.sh
+into oracle/_ref/libhiccl_ref_hip.so and launched exactly as
+`Compute<T>::start` launches it (compute.h:88-91: 256-lane workgroups,
+ceil(count / 256) of them, one launch per compute, each compute on its own
+stream, compute.h:76-78, then `wait` synchronises every stream,
+compute.h:107-117).  Test infrastructure: the checker and the yardstick,
+never the product (the product path is hiccl_amd/libhiccl_reduce.so).
+
+* bits: every fixture and inputs drawn from every f32 / bf16 bit pattern give
+  the same output words from both kernels on the same device (a NaN output's
+  payload aside), and so does the whole 1 GiB output of
+  config 2;
+* time: config 2, config 3 (n = 2 / 8 / 64), a config-4 bucket and the
+  config-5 step, interleaved; this build must not be slower on any.
+  HICCL_REF_TIMES=<file> appends each measurement as a JSON line.
+"""
+import ctypes
+import json
+import os
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import hiccl_amd
+from conftest import ROOT, bits_equal, first_mismatch, load_golden
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+REF_HIP = os.path.join(ROOT, "oracle", "_ref", "libhiccl_ref_hip.so")
+STAMP = os.path.join(ROOT, "oracle", "_ref", "BUILT_FROM_REFERENCE")
+FN = {torch.float32: "ref_hip_reduce_f32", torch.float64: "ref_hip_reduce_f64", torch.int64: "ref_hip_reduce_u64",
+      torch.int32: "ref_hip_reduce_i32", torch.bfloat16: "ref_hip_reduce_bf16"}
+TORCH_OF = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+            np.dtype(np.uint64): torch.int64, np.dtype(np.uint16): torch.bfloat16, np.dtype(np.int32): torch.int32}
+PHASE = {"engine": hiccl_amd.HICCL_ENGINE_PHASE}
+
+
+@pytest.fixture(scope="module")
+def ref():
+    if not os.path.exists(REF_HIP):
+        if os.path.exists(STAMP):
+            pytest.fail("tree built from the reference but oracle/_ref/libhiccl_ref_hip.so is missing")
+        pytest.skip("reference GPU kernel not built (tree built without /root/reference)")
+    lib = ctypes.CDLL(REF_HIP)
+    for name in FN.values():
+        f = getattr(lib, name)
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    return lib
+
+
+def ref_launch(lib, out, ins, count, stream=None):
+    """One compute as compute.h:88-91 launches it; returns the device pointer
+    table (keep it alive until the launch has run)."""
+    stream = stream or torch.cuda.current_stream()
+    tab = torch.tensor([t.data_ptr() for t in ins] or [0], dtype=torch.int64, device=DEV)
+    rc = getattr(lib, FN[out.dtype])(out.data_ptr(), count, tab.data_ptr(), len(ins), stream.cuda_stream)
+    assert rc == 0, f"reference launch failed: hipError {rc}"
+    return tab
+
+
+def to_dev(a):
+    a = np.ascontiguousarray(a)
+    t = TORCH_OF[a.dtype]
+    if a.dtype == np.uint16:
+        return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16).to(DEV)
+    if a.dtype == np.uint64:
+        return torch.from_numpy(a.view(np.int64).copy()).to(DEV)
+    return torch.from_numpy(a.copy()).to(DEV).view(t)
+
+
+def to_host(t, np_dtype):
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).cpu().numpy().view(np.uint16)
+    return t.cpu().numpy().view(np_dtype)
+
+
+def both(lib, x, np_dtype, config=None):
+    n, count = x.shape
+    ins = [to_dev(x[k]) for k in range(n)]
+    dt = TORCH_OF[np.dtype(np_dtype)]
+    a = torch.full((count,), 7, dtype=dt, device=DEV)
+    b = torch.full((count,), 9, dtype=dt, device=DEV)
+    hiccl_amd.reduce(a, ins, count=count, config=config)
+    keep = ref_launch(lib, b, ins, count)
+    torch.cuda.synchronize()
+    del keep
+    return to_host(a, np_dtype), to_host(b, np_dtype)
+
+
+def record(obj):
+    path = os.environ.get("HICCL_REF_TIMES")
+    if path:
+        with open(path, "a") as fh:
+            fh.write(json.dumps(obj) + "\n")
+    print(json.dumps(obj))
+
+
+@pytest.mark.parametrize("name,dtype", [("reduce_f32", np.float32), ("reduce_f64", np.float64),
+                                        ("reduce_u64", np.uint64), ("reduce_bf16", np.uint16),
+                                        ("reduce_i32", np.int32)])
+@pytest.mark.parametrize("cfg", [None, PHASE], ids=["auto", "phase"])
+def test_fixtures_same_bits_as_reference_gpu(ref, name, dtype, cfg):
+    for case, d in load_golden(name).items():
+        x, y = d["in"], d["out"]
+        if x.shape[0] == 0 or x.shape[1] == 0:
+            continue  # the reference kernel needs an input and an element to launch
+        ours, theirs = both(ref, x, dtype, cfg)
+        assert bits_equal(ours, theirs), f"{name}/{case}: {first_mismatch(ours, theirs)}"
+        assert bits_equal(theirs, y), f"{name}/{case}: reference GPU vs fixture: {first_mismatch(theirs, y)}"
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.uint16])
+def test_every_bit_pattern_same_as_reference_gpu(ref, dtype):
+    """Inputs drawn from all 2^32 f32 / 2^16 bf16 bit patterns (NaN, Inf,
+    denormals, signed zeros), 1-19 inputs, ragged counts up to 2^20 + 3."""
+    rng = np.random.default_rng(11)
+    nan_payload_diffs = 0
+    for it in range(24):
+        n = int(rng.integers(1, 20))
+        c = int(rng.integers(1, 5000)) if it % 4 else (1 << 20) + int(rng.integers(0, 4))
+        hi = 1 << (32 if dtype == np.float32 else 16)
+        x = rng.integers(0, hi, size=(n, c), dtype=np.uint64).astype(np.uint32 if dtype == np.float32 else np.uint16)
+        x = x.view(np.float32) if dtype == np.float32 else x
+        ours, theirs = both(ref, x, dtype)
+        assert bits_equal(ours, theirs), (n, c, first_mismatch(ours, theirs))
+        raw = np.uint32 if dtype == np.float32 else np.uint16
+        nan_payload_diffs += int(np.count_nonzero(ours.view(raw) != theirs.view(raw)))  # NaNs only, by now
+    record({"test": "every_bit_pattern", "dtype": np.dtype(dtype).name,
+            "nan_outputs_with_another_payload": nan_payload_diffs})
+
+
+def _bucket(n, count, seed=1234, dtype=torch.float32):
+    g = torch.Generator(device=DEV)
+    g.manual_seed(seed)
+    return [torch.empty(count, dtype=dtype, device=DEV).uniform_(-1, 1, generator=g) for _ in range(n)]
+
+
+def _events_ms(fn, reps):
+    s = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evs:
+        a.record(s)
+        fn()
+        b.record(s)
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in evs]
+
+
+def _one_shot_ab(lib, n, count, label, rounds=5, reps=6):
+    ins = _bucket(n, count)
+    a = torch.empty(count, device=DEV)
+    b = torch.empty(count, device=DEV)
+    tab = torch.tensor([t.data_ptr() for t in ins], dtype=torch.int64, device=DEV)
+    f = lib.ref_hip_reduce_f32
+
+    def theirs():
+        assert f(b.data_ptr(), count, tab.data_ptr(), n, torch.cuda.current_stream().cuda_stream) == 0
+
+    def ours():
+        hiccl_amd.reduce(a, ins, count=count)
+
+    ours(), theirs()
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32)), f"{label}: outputs differ"
+    t_ours, t_ref = [], []
+    for _ in range(rounds):  # interleaved, so the box's drift hits both
+        t_ours += _events_ms(ours, reps)
+        t_ref += _events_ms(theirs, reps)
+    mo, mr = float(np.median(t_ours)), float(np.median(t_ref))
+    nbytes = (n + 1) * count * 4  # compute.h:197-203
+    rec = {"test": "vs_reference_gpu_kernel", "workload": label, "n": n, "count": count,
+           "ours_ms": round(mo, 4), "reference_ms": round(mr, 4), "speedup": round(mr / mo, 3),
+           "ours_GBps": round(nbytes / mo / 1e6, 1), "reference_GBps": round(nbytes / mr / 1e6, 1),
+           "outputs_identical": True}
+    record(rec)
+    del ins, a, b, tab
+    torch.cuda.empty_cache()
+    return rec
+
+
+def test_c2_vs_reference_gpu_kernel(ref):
+    """Config 2: 8 x 2^28 fp32 (1 GiB per input); the whole output compared."""
+    rec = _one_shot_ab(ref, 8, 1 << 28, "C2: 8 x 2^28 fp32")
+    assert rec["speedup"] > 1.0, rec
+
+
+@pytest.mark.parametrize("n", [2, 8, 64])
+def test_c3_vs_reference_gpu_kernel(ref, n):
+    rec = _one_shot_ab(ref, n, 1 << 26, f"C3: {n} x 2^26 fp32")
+    assert rec["speedup"] > 1.0, rec
+
+
+def _computes_ab(lib, shapes, label, iters=200, warmup=20):
+    """Several computes per step, timed as Comm::run sees them (start + wait,
+    host clock): the reference launches one kernel per compute, each on its
+    own stream (compute.h:76-78, 88-91) and synchronises every stream
+    (compute.h:107-117); this build launches the batched plan and syncs it."""
+    comp = hiccl_amd.Compute(torch.float32, device=0)
+    streams, jobs, outs_ref, outs_ours = [], [], [], []
+    for n, count in shapes:
+        ins = _bucket(n, count, seed=n * 7 + count)
+        o1 = torch.empty(count, device=DEV)
+        o2 = torch.empty(count, device=DEV)
+        comp.add(ins, o1, count, compid=0)
+        tab = torch.tensor([t.data_ptr() for t in ins], dtype=torch.int64, device=DEV)
+        streams.append(torch.cuda.Stream(device=DEV))
+        jobs.append((ins, o2, count, n, tab))
+        outs_ours.append(o1)
+        outs_ref.append(o2)
+    f = lib.ref_hip_reduce_f32
+    torch.cuda.synchronize()
+
+    def theirs():
+        for s, (_, o2, count, n, tab) in zip(streams, jobs):
+            assert f(o2.data_ptr(), count, tab.data_ptr(), n, s.cuda_stream) == 0
+        for s in streams:
+            s.synchronize()
+
+    def ours():
+        comp.start()
+        comp.wait()
+
+    t_ours, t_ref = [], []
+    for it in range(-warmup, iters):
+        for fn, acc in ((ours, t_ours), (theirs, t_ref)):
+            t0 = time.perf_counter()
+            fn()
+            t = time.perf_counter() - t0
+            if it >= 0:
+                acc.append(t)
+    for a, b in zip(outs_ours, outs_ref):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), f"{label}: outputs differ"
+    mo, mr = float(np.median(t_ours)) * 1e6, float(np.median(t_ref)) * 1e6
+    nbytes = sum((n + 1) * c * 4 for n, c in shapes)
+    rec = {"test": "vs_reference_gpu_kernel", "workload": label, "computes": len(shapes),
+           "ours_us": round(mo, 2), "reference_us": round(mr, 2), "speedup": round(mr / mo, 3),
+           "ours_GBps": round(nbytes / mo / 1e3, 1), "reference_GBps": round(nbytes / mr / 1e3, 1),
+           "timing": "start + wait on the host clock, median", "outputs_identical": True}
+    record(rec)
+    comp.close()
+    return rec
+
+
+def test_c5_step_vs_reference_gpu_kernel(ref):
+    """The config-5 step on one rank: four 2-input and one 4-input compute of
+    2^18 floats."""
+    rec = _computes_ab(ref, [(2, 1 << 18)] * 4 + [(4, 1 << 18)], "C5 step: 4 x (2 x 2^18) + 1 x (4 x 2^18) fp32")
+    assert rec["speedup"] > 1.0, rec
+
+
+def test_c4_bucket_vs_reference_gpu_kernel(ref):
+    """Config 4 at 16 MiB per input: 8 inputs in 16 computes of 1 MiB."""
+    rec = _computes_ab(ref, [(8, 1 << 18)] * 16, "C4: 8 x 16 MiB fp32 in 16 computes of 1 MiB", iters=100)
+    assert rec["speedup"] > 1.0, rec
