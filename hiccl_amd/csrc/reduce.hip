@@ -1590,7 +1590,10 @@ int hiccl_reduce_auto_choice(int dtype, int acc, size_t count, double n, int cus
   if (!esz) return fail(hipErrorInvalidValue, "auto_choice: unknown dtype");
   if (acc != HICCL_ACC_NATIVE && acc != HICCL_ACC_WIDE) return fail(hipErrorInvalidValue, "auto_choice: bad acc");
   if (cus <= 0 || n < 0) return fail(hipErrorInvalidValue, "auto_choice: cus must be > 0 and n >= 0");
-  t_cus_override = cus;  // no device query: the choice for `cus` CUs
+  struct CusOverride {  // no device query: the choice for `cus` CUs (reset on every exit)
+    explicit CusOverride(int c) { t_cus_override = c; }
+    ~CusOverride() { t_cus_override = 0; }
+  } scoped(cus);
   hiccl_reduce_config_t z;
   memset(&z, 0, sizeof(z));
   z.acc = acc;
@@ -1600,7 +1603,6 @@ int hiccl_reduce_auto_choice(int dtype, int acc, size_t count, double n, int cus
   const uint64_t units = tiles_for(npkt, (uint64_t)c.block * c.unroll);  // tiles or phased chunks
   const uint64_t grid = std::min<uint64_t>((uint64_t)cus * c.bpc, units);
   const bool dyn = wants_dynamic(c.engine, n, units, grid, c.schedule, 0, c.unroll);
-  t_cus_override = 0;
   if (engine) *engine = c.engine;
   if (unroll) *unroll = c.unroll;
   if (blocks_per_cu) *blocks_per_cu = c.bpc;
