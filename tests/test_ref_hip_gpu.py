@@ -13,8 +13,9 @@ never the product (the product path is hiccl_amd/libhiccl_reduce.so).
   the same output words from both kernels on the same device (a NaN output's
   payload aside), and so does the whole 1 GiB output of
   config 2;
-* time: config 2, config 3 (n = 2 / 8 / 64), a config-4 bucket and the
-  config-5 step, interleaved; this build must not be slower on any.
+* time: config 2 (fp32, and its bytes in bf16), config 3 (n = 2 / 8 / 64), a
+  config-4 bucket and the config-5 step, interleaved; this build must not be
+  slower on any.
   HICCL_REF_TIMES=<file> appends each measurement as a JSON line.
 """
 import ctypes
@@ -153,12 +154,13 @@ def _events_ms(fn, reps):
     return [a.elapsed_time(b) for a, b in evs]
 
 
-def _one_shot_ab(lib, n, count, label, rounds=5, reps=6):
-    ins = _bucket(n, count)
-    a = torch.empty(count, device=DEV)
-    b = torch.empty(count, device=DEV)
+def _one_shot_ab(lib, n, count, label, rounds=5, reps=6, dtype=torch.float32):
+    ins = _bucket(n, count, dtype=dtype)
+    a = torch.empty(count, dtype=dtype, device=DEV)
+    b = torch.empty(count, dtype=dtype, device=DEV)
     tab = torch.tensor([t.data_ptr() for t in ins], dtype=torch.int64, device=DEV)
-    f = lib.ref_hip_reduce_f32
+    f = getattr(lib, FN[dtype])
+    bits = torch.int16 if dtype == torch.bfloat16 else torch.int32
 
     def theirs():
         assert f(b.data_ptr(), count, tab.data_ptr(), n, torch.cuda.current_stream().cuda_stream) == 0
@@ -168,13 +170,13 @@ def _one_shot_ab(lib, n, count, label, rounds=5, reps=6):
 
     ours(), theirs()
     torch.cuda.synchronize()
-    assert torch.equal(a.view(torch.int32), b.view(torch.int32)), f"{label}: outputs differ"
+    assert torch.equal(a.view(bits), b.view(bits)), f"{label}: outputs differ"
     t_ours, t_ref = [], []
     for _ in range(rounds):  # interleaved, so the box's drift hits both
         t_ours += _events_ms(ours, reps)
         t_ref += _events_ms(theirs, reps)
     mo, mr = float(np.median(t_ours)), float(np.median(t_ref))
-    nbytes = (n + 1) * count * 4  # compute.h:197-203
+    nbytes = (n + 1) * count * a.element_size()  # compute.h:197-203
     rec = {"test": "vs_reference_gpu_kernel", "workload": label, "n": n, "count": count,
            "ours_ms": round(mo, 4), "reference_ms": round(mr, 4), "speedup": round(mr / mo, 3),
            "ours_GBps": round(nbytes / mo / 1e6, 1), "reference_GBps": round(nbytes / mr / 1e6, 1),
@@ -188,6 +190,12 @@ def _one_shot_ab(lib, n, count, label, rounds=5, reps=6):
 def test_c2_vs_reference_gpu_kernel(ref):
     """Config 2: 8 x 2^28 fp32 (1 GiB per input); the whole output compared."""
     rec = _one_shot_ab(ref, 8, 1 << 28, "C2: 8 x 2^28 fp32")
+    assert rec["speedup"] > 1.0, rec
+
+
+def test_c2_bf16_vs_reference_gpu_kernel(ref):
+    """Config 2's bytes in bf16: 8 x 2^29 (1 GiB per input), reduce_kernel<__hip_bfloat16>."""
+    rec = _one_shot_ab(ref, 8, 1 << 29, "C2 bytes, bf16: 8 x 2^29", dtype=torch.bfloat16)
     assert rec["speedup"] > 1.0, rec
 
 
