@@ -10,12 +10,15 @@ JSON line per variant.
 """
 import ctypes
 import json
+import os
+import sys
 import time
 
 import numpy as np
 import torch
 
-import hiccl_amd
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import hiccl_amd  # noqa: E402
 
 DEV = "cuda:0"
 
