@@ -34,6 +34,8 @@ HICCL_ENGINE_PHASE = 2
 
 HICCL_PEER_STORES = 1
 HICCL_PEER_LOADS = 2
+HICCL_TOKENS_FENCED = 0  # hiccl_token_mode()
+HICCL_TOKENS_LIGHT = 1
 
 HICCL_SCHED_AUTO = 0
 HICCL_SCHED_STATIC = 1
@@ -118,6 +120,8 @@ _SIGS = {
     "hiccl_program_num_phases": (ctypes.c_int, [_vp]),
     "hiccl_program_launch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_double, _vp]),
     "hiccl_program_destroy": (None, [_vp]),
+    "hiccl_token_mode": (ctypes.c_int, []),
+    "hiccl_step_program_default": (ctypes.c_int, []),
 }
 
 

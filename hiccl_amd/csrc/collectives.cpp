@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -124,6 +125,21 @@ static int bench_json(const char *path, HiCCL::Comm<Type> &coll, Type *sendbuf_d
       if (out[i] != (Type)kat_value(i, numproc)) bad++;
   unsigned long tot = bad;
   MPI_Allreduce(MPI_IN_PLACE, &tot, 1, MPI_UNSIGNED_LONG, MPI_SUM, CommBench::comm_mpi);
+  // where each step's host time goes (Comm::set_step_timing: transport
+  // start / wait, compute launch / wait in comm.h:195-204's order, or the
+  // stream-ordered enqueue and final sync), microseconds per step, MAX over
+  // ranks of each part
+  coll.set_step_timing(true);
+  for (int r = 0; r < std::max(numiter, 1); r++) {
+    MPI_Barrier(CommBench::comm_mpi);
+    coll.run();
+  }
+  const auto sp = coll.step_split();
+  coll.set_step_timing(false);
+  const double per = sp.runs && sp.steps ? 1e6 / ((double)sp.runs * (double)sp.steps) : 0.0;
+  double split[7] = {sp.transport_start * per, sp.transport_wait * per, sp.compute_launch * per,
+                     sp.compute_wait * per, sp.finish * per, sp.enqueue * per, sp.sync * per};
+  MPI_Allreduce(MPI_IN_PLACE, split, 7, MPI_DOUBLE, MPI_MAX, CommBench::comm_mpi);
   // where the ranks ran: every rank's visible device count, its device and
   // that device's PCI bus id (a per-rank device mask that hid the other GPUs
   // shows as devices_seen 1 and repeated bus ids)
@@ -157,6 +173,7 @@ static int bench_json(const char *path, HiCCL::Comm<Type> &coll, Type *sendbuf_d
 #ifndef HICCL_PORT_HOST
     if (coll.xccl_on_rccl()) mode_used += "+xccl-rccl";
     if (coll.step_program_mode()) mode_used += "+program";
+    if (coll.stream_ordered()) mode_used += hiccl_token_mode() == HICCL_TOKENS_LIGHT ? "+tokens-light" : "+tokens-fenced";
     if (coll.shares_device()) mode_used += " (ranks share a GPU)";
 #endif
     std::string h, l;
@@ -173,13 +190,16 @@ static int bench_json(const char *path, HiCCL::Comm<Type> &coll, Type *sendbuf_d
                  "\"kernel_steps_rank0\": %d, \"kernel_ms_per_run_max_rank\": %.4f, "
                  "\"kernel_us_per_step_rank0\": %.3f, \"kernel_GBps_max_rank\": %.1f, "
                  "\"kat_exact_mismatches\": %lu, \"kat\": \"%s\", \"devices_seen\": [%s], \"rank_devices\": [%s], "
-                 "\"bus_ids\": [%s], \"mode_used\": \"%s\"}\n",
+                 "\"bus_ids\": [%s], \"mode_used\": \"%s\", \"host_split_us_per_step\": {\"transport_start\": %.3f, "
+                 "\"transport_wait\": %.3f, \"compute_launch\": %.3f, \"compute_wait\": %.3f, \"finish\": %.3f, "
+                 "\"enqueue\": %.3f, \"sync\": %.3f, \"steps\": %zu, \"runs\": %zu, \"over_ranks\": \"max\"}}\n",
                  numproc, pattern, h.c_str(), l.c_str(), pipedepth, count, data, coll.stream_ordered() ? "stream-ordered" : "host-driven",
                  coll.graph_mode() ? "+graph" : "", coll.fused_gather() ? "+fused" : "", t.t.size(), t.min() * 1e3,
                  t.median() * 1e3, t.max() * 1e3, t.median() > 0 ? data / t.median() / 1e9 : 0.0, ksteps, kmax[0],
                  ksteps ? kern_ms / ksteps * 1e3 : 0.0, kmax[0] > 0 ? kmax[1] / (kmax[0] * 1e-3) / 1e9 : 0.0, tot,
                  pattern != HiCCL::allreduce ? "n/a" : tot == 0 ? "PASSED" : "FAILED", seen.c_str(), devs.c_str(),
-                 buses.c_str(), mode_used.c_str());
+                 buses.c_str(), mode_used.c_str(), split[0], split[1], split[2], split[3], split[4], split[5], split[6],
+                 sp.steps, sp.runs);
     std::fclose(f);
   }
   return tot == 0 ? 0 : 1;

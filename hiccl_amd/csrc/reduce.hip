@@ -809,19 +809,20 @@ struct ProgArgs {
   const ProgPhase *phase;
   uint32_t *const *sig;
   const uint32_t *const *wait;
-  uint32_t *gate;  // workgroup 0 stores the launch's sequence number here after the phases
+  uint64_t *gate;  // workgroup 0 stores the launch's sequence number here after the phases
   uint32_t *err;
   const uint32_t *epoch_dev;
   uint64_t timeout_ticks;
   uint64_t nunits;
-  uint32_t stride, nphase, seq;
+  uint32_t stride, nphase;
+  uint64_t seq;  // this launch's gate value (+ *epoch_dev); never reused, see hiccl_program_launch
   uint32_t light;  // 1: relaxed token stores, no fences in the prologue (HICCL_PROG_FENCES, prog_light())
   uint32_t epoch[kProgMaxPhases];  // per launch: phase p stores / awaits epoch[p] (+ *epoch_dev)
 };
 
 // Phases [0, count) on one wave (lanes = flags), as k_sigwait_phases.
 //
-// `light` (the default, prog_light()): relaxed system-scope token stores
+// `light` (opt-in, HICCL_PROG_FENCES=light): relaxed system-scope token stores
 // and no fence after the waits.  A program's tokens never publish data of
 // their own launch -- a done token follows the copies or reductions of an
 // EARLIER launch (complete, and released, at that kernel's end; a peer's
@@ -830,8 +831,9 @@ struct ProgArgs {
 // after the gate, on workgroups whose L1 holds none of their data (the
 // kernel-start acquire invalidated it and nothing read it since).  The wave
 // issues a phase's stores only after its polls of the previous phase have
-// returned (the loop exits on the loaded value).  Full mode (release stores,
-// an acquire-release fence per phase, a release gate store) is kept for A/B.
+// returned (the loop exits on the loaded value).  Fenced mode (the default:
+// release stores, an acquire-release fence per phase, a release gate store)
+// relies on the memory model alone.
 __device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t count, uint32_t lane, uint32_t add) {
   for (uint32_t p = 0; p < count; p++) {
     const ConstU32 *q = (const ConstU32 *)&a.phase[p];
@@ -863,14 +865,17 @@ __device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t count, u
   }
 }
 
-// Bounded wait of one lane until the gate word reaches `seq` (wrap-aware);
+// Bounded wait of one lane until the gate word holds this launch's `seq`;
 // on a time-out or an error recorded by anyone it gives up (the grid drains,
 // the host reports the error).  Relaxed polls with backoff: hundreds of
-// workgroups poll one line.
-__device__ __forceinline__ void prog_gate_wait(const ProgArgs &a, uint32_t seq) {
+// workgroups poll one line.  Equality, not >=: the word holds the previous
+// launch's value until workgroup 0 stores ours, and no two launches of a
+// program share a value (64-bit, hiccl_program_launch), so a later eager
+// launch's value can never open a replay's gate early.
+__device__ __forceinline__ void prog_gate_wait(const ProgArgs &a, uint64_t seq) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint32_t nap = 1;
-  while ((int32_t)(__hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
+  while (__hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq) {
     for (uint32_t i = 0; i < nap; i++) __builtin_amdgcn_s_sleep(2);
     if (nap < 8) nap <<= 1;
     if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
@@ -917,7 +922,7 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
   for (int u = 0; u < U; u++) voff[u] = (uint32_t)((u * kProgBlock + tid) * kPacket);
   if (a.nphase) {
     const uint32_t add = a.epoch_dev ? __hip_atomic_load(a.epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    const uint32_t seq = a.seq + add;
+    const uint64_t seq = a.seq + add;
     if (blockIdx.x == 0) {
       if (tid < 64) {
         prog_phases(a, a.nphase, (uint32_t)tid, add);
@@ -948,13 +953,16 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
 
 // ------------------------------------------------------------ host side ----
 
-// HICCL_PROG_FENCES=full: release token stores and fences in the token
-// phases of programs and of k_sigwait_phases (the round-3 first version);
-// default light (prog_phases).  Read at every launch
-// (a capture keeps the value it was recorded with).
+// Token protocol of programs and of k_sigwait_phases (hiccl_token_mode).
+// Default FENCED: release token stores, acquire polls / an acquire-release
+// fence per phase, a release gate store -- the memory model's own guarantee.
+// HICCL_PROG_FENCES=light: relaxed stores and polls, no fences (prog_phases'
+// argument rests on kernel-boundary cache behaviour that only a run with one
+// GPU per rank can confirm, so it is opt-in until one has).  Read at every
+// launch (a capture keeps the value it was recorded with).
 bool prog_light() {
   const char *e = std::getenv("HICCL_PROG_FENCES");
-  return !(e && std::string(e) == "full");
+  return e && std::string(e) == "light";
 }
 
 struct DevInfo {
@@ -2231,8 +2239,8 @@ struct hiccl_program {
   std::vector<Phase> phases;  // the prologue
   bool dirty = true;
   char *d_block = nullptr;
-  uint32_t *d_gate = nullptr;
-  uint32_t seq = 0;  // last sequence number used (eager launches; captures reserve a range)
+  uint64_t *d_gate = nullptr;
+  uint64_t seq = 0;  // last sequence number used (eager launches; captures reserve a range)
   ProgArgs args;
   int unroll = 4;
   uint32_t grid = 0;
@@ -2457,9 +2465,11 @@ int hiccl_program_launch(hiccl_program_t *p, const uint32_t *epochs, const uint3
   for (uint32_t i = 0; i < a.nphase; i++) a.epoch[i] = epochs[i];
   a.light = prog_light() ? 1u : 0u;
   // the gate's sequence number: one per eager launch; a captured launch
-  // uses seq + *epoch_dev (replay r: seq + r) and reserves 2^24 of them
+  // uses seq + *epoch_dev (replay r: seq + r) and reserves every value a
+  // 32-bit *epoch_dev can add, so no later launch or re-capture of this
+  // program reuses a value one of its replays stores (64-bit: no wrap)
   a.seq = ++p->seq;
-  if (epoch_dev) p->seq += (1u << 24);
+  if (epoch_dev) p->seq += (1ull << 32);
   fn(a, dim3(p->grid), s);
   p->enqueued.store(true, std::memory_order_relaxed);
   return check_hip(hipGetLastError(), "program_launch: launch");
@@ -2472,6 +2482,13 @@ void hiccl_program_destroy(hiccl_program_t *p) {
   if (p->d_block) (void)hipFree(p->d_block);
   if (p->d_gate) (void)hipFree(p->d_gate);
   delete p;
+}
+
+int hiccl_token_mode(void) { return prog_light() ? HICCL_TOKENS_LIGHT : HICCL_TOKENS_FENCED; }
+
+int hiccl_step_program_default(void) {
+  const char *e = std::getenv("HICCL_STEP_PROGRAM");
+  return e && std::string(e) == "1";
 }
 
 // ---------------------------------------------------------- measurement --

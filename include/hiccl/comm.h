@@ -280,6 +280,11 @@ class Comm {
                   steps.size(), libs.size(), streamed ? "stream-ordered" : "host-driven", graphed ? ", graph replay" : "",
                   fused ? ", fused gather" : "", xccl ? ", XCCL on RCCL" : "");
 #ifndef HICCL_PORT_HOST
+    if (streamed && CommBench::myid == CommBench::printid)
+      std::printf("stream-ordered protocol: %s tokens, %s\n",
+                  hiccl_token_mode() == HICCL_TOKENS_LIGHT ? "light (relaxed, HICCL_PROG_FENCES=light)"
+                                                           : "fenced (release / acquire)",
+                  programs ? "step programs (HICCL_STEP_PROGRAM=1)" : "one launch per element");
     if (programs && CommBench::myid == CommBench::printid) std::printf("step programs: token phases folded into the step's launches\n");
 #endif
   }
@@ -303,6 +308,7 @@ class Comm {
     std::vector<typename std::list<Command<T>>::iterator> it(nl);
     for (size_t i = 0; i < nl; i++) it[i] = command_batch[i].begin();
     if (nl == 0) return;
+    if (timing) return run_timed(it);
     while (it[0] != command_batch[0].end()) {  // every library has one command per step
       for (size_t i = 0; i < nl; i++) it[i]->comm->start();
       for (size_t i = nl; i-- > 0;) {
@@ -316,6 +322,24 @@ class Comm {
       }
     }
   }
+
+  // Host wall time of run() split by what the host waits on, per step, in
+  // comm.h:186-206's order: host-driven -- transport start, transport wait,
+  // compute launch, compute wait (comm.h:195-204), and the fused transfers'
+  // release; stream-ordered -- enqueueing the pipeline (or launching its
+  // graph) and the one synchronisation at the end.  Seconds, summed over the
+  // runs since set_step_timing(true); `steps` = pipeline steps per run.
+  struct StepSplit {
+    double transport_start = 0, transport_wait = 0, compute_launch = 0, compute_wait = 0, finish = 0;
+    double enqueue = 0, sync = 0;
+    size_t runs = 0, steps = 0;
+  };
+  void set_step_timing(bool on) {
+    timing = on;
+    split = StepSplit{};
+    split.steps = steps.size();
+  }
+  const StepSplit &step_split() const { return split; }
 
   // comm.h:208-212
   void run(T *sb, T *rb) {
@@ -420,6 +444,40 @@ class Comm {
   pthread_t thread{};
   bool running = false;
 
+  bool timing = false;
+  StepSplit split;
+
+  // run() with the host wall split recorded (set_step_timing): the same calls
+  // in the same order, a clock read between them.
+  template <class It>
+  void run_timed(std::vector<It> &it) {
+    const size_t nl = it.size();
+    double t = MPI_Wtime();
+    auto lap = [&t](double &acc) {
+      const double u = MPI_Wtime();
+      acc += u - t;
+      t = u;
+    };
+    while (it[0] != command_batch[0].end()) {
+      for (size_t i = 0; i < nl; i++) it[i]->comm->start();
+      lap(split.transport_start);
+      for (size_t i = nl; i-- > 0;) {
+        it[i]->comm->wait();
+        lap(split.transport_wait);
+        it[i]->compute->start();
+        lap(split.compute_launch);
+      }
+      for (size_t i = 0; i < nl; i++) it[i]->compute->wait();
+      lap(split.compute_wait);
+      for (size_t i = 0; i < nl; i++) {
+        it[i]->comm->finish();
+        ++it[i];
+      }
+      lap(split.finish);
+    }
+    split.runs++;
+  }
+
   int stream_req = -1;  // -1: decide from the environment and the node layout; 2: forced
   bool streamed = false;
   bool shared_device = false;  // two or more ranks drive one GPU
@@ -439,6 +497,7 @@ class Comm {
     CommBench::setup_gpu();
     hipStream_t s = CommBench::transport_stream();
     if (command_batch.empty()) return;
+    const double t0 = timing ? MPI_Wtime() : 0.0;
     if (graphed && ran_eager) {
       if (gexec && !epochs_match()) drop_graph();  // eager executions since (measure): re-record
       if (!gexec) capture(s);
@@ -450,7 +509,13 @@ class Comm {
       ran_eager = true;
     }
     CommBench::flush_signals();
+    const double t1 = timing ? MPI_Wtime() : 0.0;
     CommBench::hip_check(hipStreamSynchronize(s), "run: stream sync");
+    if (timing) {
+      split.enqueue += t1 - t0;
+      split.sync += MPI_Wtime() - t1;
+      split.runs++;
+    }
     if (*flags.err) CommBench::die("run", "stream-ordered signal timed out (a peer never signalled)");
   }
 
@@ -470,8 +535,8 @@ class Comm {
     CommBench::flush_signals();  // (the last step's done tokens)
   }
 
-  // Programs (HICCL_STEP_PROGRAM; stream-ordered mode, on by default with one
-  // GPU per rank, want_programs()): the
+  // Programs (HICCL_STEP_PROGRAM=1; stream-ordered mode, opt-in,
+  // want_programs()): the
   // first stream-ordered run() records the enqueue sequence above -- per
   // step every library's ready tokens, copies and done tokens, the computes
   // in reverse library order, the fused transfers' done tokens -- as a list
@@ -512,6 +577,7 @@ class Comm {
         for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue_copies(s);
         for (size_t i = 0; i < nl; i++) it[i]->comm->enqueue_post(s);
         for (size_t i = nl; i-- > 0;) it[i]->compute->launch(s);
+        rec.end_step();
         for (size_t i = 0; i < nl; i++) {
           it[i]->comm->enqueue_tail(s);
           ++it[i];
@@ -544,16 +610,19 @@ class Comm {
     return std::max(8, cus / device_ranks);
   }
 
-  // Default: programs when every rank drives its own GPU.  Ranks sharing one
-  // GPU (forced single-GPU rehearsals) launch per element unless
-  // HICCL_STEP_PROGRAM=1: a program's workgroups wait on the device for the
-  // peer's token while the peer's kernels need that device to produce it
-  // (2 ranks, pipedepth 128, 64 MiB/rank: graph + fused 2.67-2.93 ms with
-  // programs vs 1.57-1.58 without, profiles/r03i_c5_prog_ab.jsonl; one
-  // process per GPU: 15.2 vs 22.1 us per step, profiles/r03g_progstep.jsonl).
+  // Default: OFF (hiccl_step_program_default(); HICCL_STEP_PROGRAM=1 opts
+  // in), whatever the device layout.  Programs were measured only with ranks
+  // sharing one GPU, where they lose (a program's workgroups wait on the
+  // device for the peer's token while the peer's kernels need that device to
+  // produce it: 2 ranks, pipedepth 128, 64 MiB/rank, graph + fused 2.67-2.93
+  // ms with programs vs 1.57-1.58 without, profiles/r03i_c5_prog_ab.jsonl),
+  // and in a one-process enqueue probe, where they win (15.2 vs 22.1 us per
+  // step, profiles/r03g_progstep.jsonl).  With one GPU per rank a program's
+  // gate-waiting grid also occupies every CU while ranks are out of step, so
+  // the per-element launches the GPU suite verifies stay the default until an
+  // 8-GPU run (bench.py's config-5 leg carries the A/B) decides.
   bool want_programs() {
-    const char *env = std::getenv("HICCL_STEP_PROGRAM");
-    int on = env ? std::string(env) != "0" : device_ranks <= 1;
+    int on = hiccl_step_program_default();
     for (auto &lst : command_batch)
       for (auto &c : lst) on = on && c.comm->recordable();
     MPI_Allreduce(MPI_IN_PLACE, &on, 1, MPI_INT, MPI_LAND, CommBench::comm_mpi);

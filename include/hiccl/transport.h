@@ -756,6 +756,11 @@ struct StepRecorder {
     if (hiccl_program_create(&cur, dtype, device)) die("program", hiccl_last_error());
     if (max_wg && hiccl_program_set_max_workgroups(cur, max_wg)) die("program", hiccl_last_error());
   }
+  // A step's computes are complete: the next step's computes start a new
+  // batch even when nothing of this rank is recorded between them (a step
+  // with computes but no phase or copy of its own) -- the reference waits
+  // for each step's computes before the next step starts (comm.h:203-204).
+  void end_step() { last = 0; }
   void close() {
     if (!cur) return;
     launches.push_back(Launch{cur, std::move(cur_epochs)});

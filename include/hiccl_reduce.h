@@ -286,10 +286,10 @@ void hiccl_host_pipe_destroy(hiccl_host_pipe_t *pipe);
  * of `epoch` to each of the nsig flags `sig` (typically flags in a peer's
  * IPC-mapped device memory), then a bounded spin until each of the nwait
  * local flags `wait` holds a value >= epoch (32-bit wrap-aware).  The
- * stores and polls are relaxed (HICCL_PROG_FENCES=full: release stores,
- * acquire polls): a token orders launches and publishes nothing of its own
- * launch, so data it announces must be complete when the launch that wrote
- * it ended -- written through to a peer's memory with
+ * stores are system-scope releases and the polls acquires
+ * (hiccl_token_mode; HICCL_PROG_FENCES=light makes both relaxed).  A token
+ * orders launches; data it announces must be complete when the launch that
+ * wrote it ended -- written through to a peer's memory with
  * hiccl_reduce_plan_set_peer.  A spin exceeding timeout_s (<= 0: 30 s) stores
  * 1 to *err (if err is not NULL; host-visible memory recommended) and gives
  * up instead of hanging.  Replaces, per pipeline step, the host round trip
@@ -335,7 +335,7 @@ int hiccl_signal_wait_phases(const hiccl_signal_phase_t *phases, int nphases, co
  * computes -- plans' computes, reductions of the program's dtype or
  * HICCL_BYTES exact copies, all independent of each other -- which start
  * only after the last phase.  Same stores, waits and results as the
- * separate launches (the same relaxed tokens), one kernel boundary fewer
+ * separate launches (the same token mode), one kernel boundary fewer
  * per phase group.
  *
  * add_signal appends one phase (only before the first add_plan); its epoch
@@ -365,6 +365,25 @@ int hiccl_program_num_phases(const hiccl_program_t *prog);
 int hiccl_program_launch(hiccl_program_t *prog, const uint32_t *epochs, const uint32_t *epoch_dev, uint32_t *err,
                          double timeout_s, void *stream);
 void hiccl_program_destroy(hiccl_program_t *prog);
+
+/* Stream-ordered protocol defaults, resolved from the environment at each
+ * call (launches resolve them the same way; no device needed).
+ *   hiccl_token_mode: the token phases of hiccl_signal_wait* and programs.
+ *     HICCL_TOKENS_FENCED (default; HICCL_PROG_FENCES unset, "full" or any
+ *     other value): system-scope release token stores, acquire polls, an
+ *     acquire-release fence per phase, a release gate store -- ordering by the
+ *     memory model alone.  HICCL_TOKENS_LIGHT (HICCL_PROG_FENCES=light):
+ *     relaxed stores and polls, no fences; 0.4-4.5 us cheaper per step on one
+ *     GPU, but its argument (tokens publish nothing of their own launch) leans
+ *     on kernel-boundary cache behaviour across GPUs that no run with one GPU
+ *     per rank has confirmed yet, so it is opt-in.
+ *   hiccl_step_program_default: 1 when HiCCL::Comm's stream-ordered mode folds
+ *     token phases into step programs (HICCL_STEP_PROGRAM=1), else 0 -- one
+ *     launch per element, the protocol the GPU suite verifies by default. */
+#define HICCL_TOKENS_FENCED 0
+#define HICCL_TOKENS_LIGHT 1
+int hiccl_token_mode(void);
+int hiccl_step_program_default(void);
 
 /* ----------------------------------------------------------------------
  * Measurement utilities (bench.py; not part of the reference surface).

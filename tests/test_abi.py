@@ -185,3 +185,23 @@ def test_auto_choice_rule_table_on_host():
     import ctypes
     assert lib.hiccl_reduce_auto_choice(42, 0, 1024, 2.0, 256, None, None, None, None) == 1
     assert lib.hiccl_reduce_auto_choice(f32, 0, 1024, 2.0, 0, None, None, None, None) == 1
+
+
+def test_stream_ordered_defaults_resolve_as_stated(monkeypatch):
+    """The stream-ordered protocol defaults: fenced
+    token phases unless HICCL_PROG_FENCES=light, one launch per element
+    unless HICCL_STEP_PROGRAM=1 -- resolved from the environment at each call,
+    as every launch resolves them (hiccl_token_mode,
+    hiccl_step_program_default; HiCCL::Comm::want_programs uses the latter)."""
+    lib = L.lib()
+    for k in ("HICCL_PROG_FENCES", "HICCL_STEP_PROGRAM"):
+        monkeypatch.delenv(k, raising=False)
+    assert lib.hiccl_token_mode() == L.HICCL_TOKENS_FENCED
+    assert lib.hiccl_step_program_default() == 0
+    for v, want in (("full", L.HICCL_TOKENS_FENCED), ("light", L.HICCL_TOKENS_LIGHT), ("", L.HICCL_TOKENS_FENCED),
+                    ("LIGHT", L.HICCL_TOKENS_FENCED), ("0", L.HICCL_TOKENS_FENCED)):
+        monkeypatch.setenv("HICCL_PROG_FENCES", v)
+        assert lib.hiccl_token_mode() == want, v
+    for v, want in (("1", 1), ("0", 0), ("", 0), ("yes", 0)):
+        monkeypatch.setenv("HICCL_STEP_PROGRAM", v)
+        assert lib.hiccl_step_program_default() == want, v

@@ -122,6 +122,8 @@ def test_cpu_leg_full_bucket_parity(tmp_path):
         r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
         assert r["parity_full"]["ok"] is ok and r["parity_full"]["mismatches"] == mism
         assert r["threads"] == 2 and "OMP_PROC_BIND=spread" in r["sample"]
+        # the spread over the passes: min <= median (value) <= max, one time per pass
+        assert r["min"] <= r["value"] <= r["max"] and r["passes"] == len(r["pass_ms"]) >= 1
 
 
 def test_serial_rw_model():
@@ -181,3 +183,12 @@ def test_c5_driver_json_records_devices_and_mode(tmp_path):
     assert r["devices_seen"] == [0, 0] and r["rank_devices"] == [-1, -1]
     assert r["bus_ids"] == ["host", "host"]
     assert r["mode_used"] == "host-driven"
+    # the per-step host wall split, in comm.h:195-204's order (host-driven:
+    # transport start / wait, compute launch / wait; the stream-ordered
+    # parts stay 0 here), MAX over ranks
+    hs = r["host_split_us_per_step"]
+    assert hs["steps"] >= 4 and hs["runs"] == 2 and hs["over_ranks"] == "max"
+    for k in ("transport_start", "transport_wait", "compute_launch", "compute_wait", "finish"):
+        assert hs[k] >= 0.0, k
+    assert hs["transport_wait"] + hs["compute_wait"] > 0.0
+    assert hs["enqueue"] == 0.0 and hs["sync"] == 0.0

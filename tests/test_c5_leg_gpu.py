@@ -22,9 +22,10 @@ def test_c5_leg_rehearsal_one_gpu(ranks):
     import bench
     res = bench.run_c5(ranks, argparse.Namespace(c5_log2count=14, c5_iters=2), allow_shared=True)
     assert "workload" in res, res
-    modes = (["host", "stream_graph", "stream_graph_fused", "stream_graph_fused_noprog", "xccl"]
-             + (["flat_stream_graph_fused"] if ranks > 2 else []))
-    assert [m for m in res if m.endswith(("host", "fused", "graph", "xccl", "noprog"))] == modes
+    # the verified default protocol first, the light-token programs last
+    modes = (["host", "stream_graph", "stream_graph_fused_noprog", "stream_graph_fused_fenced"]
+             + (["flat_stream_graph_fused"] if ranks > 2 else []) + ["xccl", "stream_graph_fused"])
+    assert [m for m in res if m.endswith(("host", "fused", "graph", "xccl", "noprog", "fenced"))] == modes
     assert res["devices_counted_unmasked"] >= 1 and isinstance(res["env_scrubbed"], dict)
     for mode in modes:
         r = res[mode]
@@ -37,3 +38,9 @@ def test_c5_leg_rehearsal_one_gpu(ranks):
         assert r["hierarchy"] == (str(ranks) if mode.startswith("flat") or ranks == 2 else f"1,{ranks // 2},2")
         assert r["collective_ms_median"] > 0 and r["algorithmic_GBps_median"] > 0
         assert r["kernel_steps_rank0"] > 0 and r["kernel_ms_per_run_max_rank"] > 0
+        hs = r["host_split_us_per_step"]  # shared GPU: host-driven, the transport / compute parts
+        assert hs["steps"] > 0 and hs["runs"] == 2 and hs["transport_wait"] + hs["compute_wait"] > 0
+    ab = res["protocol_ab"]
+    assert ab["baseline_kat"] == "PASSED" and ab["baseline_ms"] > 0
+    for name in ("stream_graph_fused_fenced", "stream_graph_fused"):
+        assert ab[name]["kat"] == "PASSED" and ab[name]["over_baseline"] > 0

@@ -33,17 +33,17 @@ def mpirun(np_, exe, args, timeout=180, streamed=True, fused=False, engine="auto
     """streamed: HICCL_STREAM_ORDERED=force -- every rank here shares the box's
     one GPU, where the library would otherwise fall back to host-driven mode
     (tested by test_shared_device_falls_back_to_host_driven).  Stream-ordered
-    runs ask for step programs (HICCL_STEP_PROGRAM=1), the default with one
-    GPU per rank, which ranks sharing a GPU would otherwise not use
-    (test_shared_device_defaults_to_per_element_launches); extra_env wins."""
+    runs take the library's default protocol -- fenced tokens, one launch per
+    element (test_stream_ordered_default_protocol) -- unless extra_env sets
+    HICCL_STEP_PROGRAM / HICCL_PROG_FENCES; extra_env wins, None unsets."""
     assert np_ <= 8
     if stream_env is None:
         stream_env = "force" if streamed else "0"
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", HICCL_STREAM_ORDERED=stream_env,
                HICCL_FUSED_GATHER="1" if fused else "0", HICCL_SIGNAL_TIMEOUT="10", HICCL_ENGINE=engine,
                HICCL_GRAPH="1" if graph else "0", HICCL_DRIVER_REPEAT=str(repeat))
-    if streamed:
-        env["HICCL_STEP_PROGRAM"] = "1"
+    for k in ("HICCL_STEP_PROGRAM", "HICCL_PROG_FENCES"):  # the defaults unless asked
+        env.pop(k, None)
     for k, v in (extra_env or {}).items():  # None: unset
         if v is None:
             env.pop(k, None)
@@ -127,16 +127,21 @@ def test_allreduce_float_bits_vs_oracle(tmp_path, oracle, np_, count, stripe, ri
 
 @pytest.mark.parametrize("np_,count,depth,hier,libs", [(2, 65536, 4, "2", "ipc"), (8, 4099, 4, "1,4,2", "mpi,ipc,ipc")])
 @pytest.mark.parametrize("fused,graph", [(False, False), (True, True)], ids=["stream", "stream-fused-graph"])
-@pytest.mark.parametrize("program", ["0", "1"], ids=["per_element", "step_program"])
-def test_allreduce_bits_step_program_ab(tmp_path, oracle, np_, count, depth, hier, libs, fused, graph, program):
-    """Stream-ordered mode with one step program per pipeline step (the
-    default) and with one launch per element
-    (HICCL_STEP_PROGRAM=0): the same bits as oracle/schedule.py either way."""
+@pytest.mark.parametrize("program,tokens", [("0", "full"), ("1", "full"), ("1", "light"), ("0", "light")],
+                         ids=["per_element-fenced", "step_program-fenced", "step_program-light", "per_element-light"])
+def test_allreduce_bits_step_program_ab(tmp_path, oracle, np_, count, depth, hier, libs, fused, graph, program,
+                                        tokens):
+    """Stream-ordered mode under every protocol the config-5 leg A/Bs: one
+    launch per element or one step program per step (HICCL_STEP_PROGRAM),
+    with fenced or light token phases (HICCL_PROG_FENCES, hiccl_token_mode):
+    the same bits as oracle/schedule.py every way."""
     prefix = str(tmp_path / "ar")
     rc, out = mpirun(np_, HIP_F32, [8, count, 1, 1, depth, 0, 0, hier, libs, prefix], streamed=True, fused=fused,
-                     graph=graph, repeat=4 if graph else 2, extra_env={"HICCL_STEP_PROGRAM": program})
+                     graph=graph, repeat=4 if graph else 2,
+                     extra_env={"HICCL_STEP_PROGRAM": program, "HICCL_PROG_FENCES": tokens})
     assert rc == 0, out[-3000:]
     assert ("step programs: token phases folded" in out) == (program == "1"), out[-2000:]
+    assert ("light (relaxed" if tokens == "light" else "fenced (release") in out, out[-2000:]
     n = count * np_
     x = {r: oracle.fill(r + 1, n, 1234)[r] for r in range(np_)}
     libmap = {"mpi": S.MPI, "ipc": S.IPC, "ipc_get": S.IPC_GET}
@@ -156,16 +161,16 @@ def test_allreduce_bits_step_program_ab(tmp_path, oracle, np_, count, depth, hie
 
 
 @pytest.mark.parametrize("graph", [False, True], ids=["stream", "stream-graph"])
-def test_shared_device_defaults_to_per_element_launches(graph):
-    """Ranks sharing the GPU, stream-ordered forced, HICCL_STEP_PROGRAM unset:
-    one launch per element of a step (a program's waiting workgroups would
-    hold the device the peer needs, profiles/r03i_c5_prog_ab.jsonl); the KAT
-    passes."""
-    rc, out = mpirun(2, HIP, [8, 4099, 1, 1, 3, 0, 0, "2", "ipc"], graph=graph,
-                     extra_env={"HICCL_STEP_PROGRAM": None})
+def test_stream_ordered_default_protocol(graph):
+    """Stream-ordered, HICCL_STEP_PROGRAM and HICCL_PROG_FENCES unset: the
+    default protocol is fenced tokens and one launch per element of a step
+    (the verified one; programs and light tokens are opt-in until a run with
+    one GPU per rank decides); init says so and the KAT passes."""
+    rc, out = mpirun(2, HIP, [8, 4099, 1, 1, 3, 0, 0, "2", "ipc"], graph=graph)
     assert rc == 0, out[-3000:]
     assert "PASSED!" in out and "stream-ordered" in out
-    assert "step programs" not in out, out[-2000:]
+    assert "stream-ordered protocol: fenced (release / acquire) tokens, one launch per element" in out, out[-2000:]
+    assert "step programs: token phases folded" not in out, out[-2000:]
 
 
 @pytest.mark.parametrize("np_,hier,libs", [(2, "2", "ipc"), (4, "2,2", "mpi,ipc"), (4, "4", "ipc_get"),

@@ -49,6 +49,28 @@ def test_config1_two_rank_reduce_float():
     assert "VERIFY REDUCE ROOT = 0: PASSED!" in out
 
 
+@pytest.mark.gpu
+def test_config1_two_rank_reduce_float_on_gpu_box_host(tmp_path, oracle):
+    """Config 1 exactly as BASELINE.json names it (Comm<float> add_reduction of
+    2 x 1 MiB, 2 MPI ranks, CPU sum path) on the GPU box's own host -- the
+    box the CPU baseline is timed on.  Marked gpu so the round-end GPU tier
+    records it there; no GPU is used.  Besides the reference's KAT, the root's
+    float result must equal, bit for bit, the oracle's in-order sum of the two
+    ranks' generator inputs (rank 0 + rank 1, the flat order reduce.h:134-169
+    emits)."""
+    rc, out = mpirun(2, HOST_F32, [4, 131072, 1, 1, 1, 1, 3])
+    assert rc == 0, out
+    assert "VERIFY REDUCE ROOT = 0: PASSED!" in out
+    prefix = str(tmp_path / "c1")
+    rc, out = mpirun(2, HOST_F32, [4, 131072, 1, 1, 1, 0, 0, "2", "mpi", prefix])
+    assert rc == 0, out
+    n = 131072 * 2
+    x = [oracle.fill(r + 1, n, 1234)[r] for r in range(2)]  # rank r's input, as the driver generates it
+    got = np.fromfile(f"{prefix}.rank0.bin", dtype=np.float32)
+    exp = oracle.reduce(x)  # pattern 4: root 0 receives the sum of both 1 MiB send buffers
+    assert len(got) == n and got.tobytes() == exp.tobytes()
+
+
 @pytest.mark.parametrize("np_,hier,libs", [(2, "2", "mpi"), (4, "2,2", "mpi,ipc"), (8, "1,4,2", "mpi,ipc,ipc"),
                                            (6, "3,2", "mpi,mpi")])
 @pytest.mark.parametrize("pattern", range(1, 9))

@@ -235,6 +235,79 @@ def test_graph_replay_reads_epoch_counter():
     prog.close()
 
 
+def test_gate_values_never_reused_across_captures():
+    """The gate word a replay leaves behind never opens a later capture's gate
+    early.  Graph A is replayed with its epoch counter far ahead (as after
+    2^24 + 11 replays), so its gate value is high; graph B, captured next
+    from the same program with a fresh counter, must still keep its units
+    back until its phase is satisfied (the host plays the peer, as in
+    test_units_wait_for_the_phases).  With 32-bit gate values reserved 2^24
+    per capture and a >= test, B's workgroups passed the gate at once."""
+    import time
+    count = (1 << 18) + 3
+    nb = count * 4
+    sp, free_s = _host_coherent(nb)
+    dp, free_d = _host_coherent(nb)
+    fp, free_f = _host_coherent(256)
+    src_np = np.ctypeslib.as_array((ctypes.c_float * count).from_address(sp))
+    dst_np = np.ctypeslib.as_array((ctypes.c_float * count).from_address(dp))
+    flag_np = np.ctypeslib.as_array((ctypes.c_int32 * 64).from_address(fp))
+    flag_np[:] = 0
+    src, dst = torch.from_numpy(src_np), torch.from_numpy(dst_np)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    cp = _copy_plan(dst, src, nb)
+    prog = hiccl_amd.Program(torch.float32, device=0)
+    prog.add_signal([], [fp])
+    prog.add_plan(cp)
+    ctr_a = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ctr_b = torch.zeros(1, dtype=torch.int32, device=DEV)
+    s = torch.cuda.Stream()
+
+    def capture(ctr, epoch):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                cs = torch.cuda.current_stream()
+                L.check(L.lib().hiccl_counter_add(ctypes.c_void_p(ctr.data_ptr()), 1,
+                                                  ctypes.c_void_p(cs.cuda_stream)), "counter_add")
+                prog.launch([epoch], epoch_dev=ctr.data_ptr(), err=err.data_ptr(), timeout_s=20.0, stream=cs)
+        return g
+
+    try:
+        flag_np[0] = 1
+        prog.launch([1], err=err.data_ptr(), timeout_s=20.0)  # eager: uploads
+        torch.cuda.synchronize()
+        ga = capture(ctr_a, 10)
+        ctr_a.fill_((1 << 24) + 10)  # replay A as its (2^24 + 11)-th
+        flag_np[0] = 10 + (1 << 24) + 11
+        ga.replay()
+        torch.cuda.synchronize()
+        assert err.item() == 0
+        base = 1 << 25  # B's token epochs: above every flag value so far
+        gb = capture(ctr_b, base)
+        rng = np.random.default_rng(5)
+        for r in range(1, 3):
+            src_np[:] = rng.standard_normal(count, dtype=np.float32)
+            dst_np[:] = np.nan
+            gb.replay()
+            time.sleep(0.05)
+            assert np.isnan(dst_np).all(), f"replay {r} of B: a unit ran before its gate opened"
+            new = rng.standard_normal(count, dtype=np.float32)
+            src_np[:] = new
+            flag_np[0] = base + r
+            torch.cuda.synchronize()
+            assert err.item() == 0
+            assert np.array_equal(dst_np.view(np.int32), new.view(np.int32)), f"replay {r} of B: stale source"
+        del ga, gb
+    finally:
+        torch.cuda.synchronize()
+        prog.close()
+        cp.close()
+        free_s()
+        free_d()
+        free_f()
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float64, torch.int64], ids=["bf16", "f64", "u64"])
 def test_program_dtypes_match_oracle(oracle, dtype):
     count = (1 << 17) + 9

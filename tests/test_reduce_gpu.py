@@ -689,12 +689,17 @@ def test_config3_exact_sizes(oracle, n):
     assert ok, msg
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
-def test_config4_exact_256MiB_in_1MiB_computes(oracle, dtype):
-    """Config 4: n = 8, 256 MiB per input split into 1 MiB computes with the
-    partition() formula (reduce.h:401-415), ONE batched plan launch."""
+def _config4_bucket(oracle, dtype, per_input):
+    """Config 4: n = 8, `per_input` bytes per input split into 1 MiB computes
+    with the partition() formula (reduce.h:401-415; pipedepth = bytes / 1 MiB,
+    as SURVEY.md 8d C4), ONE batched plan launch; checked at a random sample,
+    at every compute's first and last element against the oracle generator,
+    and for no element left unwritten (the output starts as NaN)."""
     n, esz = 8, (2 if dtype == torch.bfloat16 else 4)
-    count, seed, depth = (256 << 20) // esz, 4000 + esz, 256
+    count, seed, depth = per_input // esz, 4000 + esz + (per_input >> 28), per_input >> 20
+    free, _ = torch.cuda.mem_get_info()
+    if free < (n + 1) * per_input + (1 << 30):
+        pytest.skip("not enough device memory")
     ins = [torch.empty(count, dtype=dtype, device=DEV) for _ in range(n)]
     for k, t in enumerate(ins):
         hiccl_amd.fill_uniform(t, seed, k)
@@ -705,16 +710,33 @@ def test_config4_exact_256MiB_in_1MiB_computes(oracle, dtype):
         c = count // depth + (1 if b < count % depth else 0)
         comp.add([(t, off) for t in ins], (out, off), c, compid=0)
         off += c
-    assert off == count
+    assert off == count and comp.numcomp == depth
     comp.start(stream=torch.cuda.current_stream())
     torch.cuda.synchronize()
-    # every compute's first and last element, plus the random sample
     bounds = [b * (count // depth) + min(b, count % depth) for b in range(depth)]
     ok, msg = _sampled(out, n, count, seed, bf16=(dtype == torch.bfloat16),
-                       extra=bounds + [x - 1 for x in bounds[1:]])
+                       extra=bounds + [x - 1 for x in bounds[1:]] + [count - 1])
     assert ok, msg
-    assert not torch.isnan(out.float()).any().item()  # no compute left unwritten
+    assert not torch.isnan(out).any().item()  # no compute left unwritten
     comp.close()
+    del ins, out
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_config4_exact_256MiB_in_1MiB_computes(oracle, dtype):
+    """Config 4 at 256 MiB per input: 256 computes of 1 MiB in one launch."""
+    _config4_bucket(oracle, dtype, 256 << 20)
+
+
+@pytest.mark.parametrize("per_input", [1 << 30, 4 << 30], ids=["1GiB", "4GiB"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_config4_large_in_1MiB_computes(oracle, dtype, per_input):
+    """Config 4's largest sizes: 1 GiB and 4 GiB per input = 1,024 and 4,096
+    computes of 1 MiB in ONE plan launch -- at 4 GiB the computes' byte
+    offsets pass 2^32 inside the batched plan (bf16: 2^31 elements per
+    input)."""
+    _config4_bucket(oracle, dtype, per_input)
 
 
 def test_bf16_2pow31_elements_64bit_offsets(oracle):

@@ -21,7 +21,7 @@ __device__ __forceinline__ rsrc_t mk(const void *p, uint32_t n) {
 }
 
 struct Ptrs {
-  const char *in[16];
+  const char *in[64];
   char *out;
   uint64_t bytes;  // per stream
   int n;
@@ -205,10 +205,11 @@ extern "C" {
 // mode: 0 mix (N reads + 1 write), 1 read-only, 2 write-only, 3 LDS-DMA mix
 int probe_run(int mode, int block, int unroll, int aux_load, int aux_store, int order, int grid,
               const void *const *in, int n, void *out, uint64_t bytes, void *stream) {
-  // the kernels read p.in[0..n): at most 16 streams (8 for the LDS mix)
-  if (n < 1 || n > 16 || (mode == 3 && n > 8)) return -1;
+  // the kernels read p.in[0..n): at most 64 streams (8 for the LDS and
+  // grouped mixes), as many as config 3's largest bucket
+  if (n < 1 || n > 64 || (mode == 3 && n > 8)) return -1;
   Ptrs p;
-  for (int k = 0; k < 16; k++) p.in[k] = (const char *)(k < n ? in[k] : in[0]);
+  for (int k = 0; k < 64; k++) p.in[k] = (const char *)(k < n ? in[k] : in[0]);
   p.out = (char *)out;
   p.bytes = bytes;
   p.n = n;
