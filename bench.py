@@ -1581,9 +1581,13 @@ def roundtrip(args):
             out[name]["parity_ok"] = bool(torch.equal(host_out.view(torch.int32), expect.view(torch.int32)))
     for p in pipes.values():
         p.close()
-    # device-only reference
+    # device-only reference, and the link alone: the n inputs H2D, the output D2H
     _, ms = time_launches(lambda: hiccl_amd.reduce(dev_out, dev_in), 10, 3)
     out["kernel_only_GBps"] = round((n + 1) * count * 4 / (np.median(ms) * 1e-3) / 1e9, 1)
+    wall, _ = time_launches(lambda: [d.copy_(h, non_blocking=True) for h, d in zip(host_in, dev_in)], 3, 1)
+    out["h2d_only_GBps"] = round(n * count * 4 * 3 / wall / 1e9, 2)
+    wall, _ = time_launches(lambda: host_out.copy_(dev_out, non_blocking=True), 3, 1)
+    out["d2h_only_GBps"] = round(count * 4 * 3 / wall / 1e9, 2)
     pipelined()
     torch.cuda.synchronize()
     exp = expect
