@@ -5,7 +5,7 @@ shape = the engine AUTO picked), its rocprofv3 average duration and rate,
 HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of
 MI355X_MICROARCH.md), and the SQ occupancy / stall fractions.
 
-    python tools/c3_pmc_summary.py <tag>
+    python tools/c3_pmc_summary.py <tag> [n ...]   (default: every n measured)
 """
 import csv
 import glob
@@ -35,8 +35,11 @@ def main():
     tag = sys.argv[1]
     res = {"tag": tag, "workload": "C3: n inputs x 2^26 fp32 (256 MiB/input), AUTO engine, bench.py --n N --log2count 26",
            "per_n": {}}
+    only = {int(x) for x in sys.argv[2:]}
     for d in sorted(glob.glob(os.path.join(ROOT, "gpurun_out", "c3pmc", "n*")), key=lambda p: int(p.rsplit("n", 1)[1])):
         n = int(d.rsplit("n", 1)[1])
+        if only and n not in only:
+            continue
         count = 1 << 26
         alg = (n + 1) * count * 4
         row = {"algorithmic_bytes_per_launch": alg}
