@@ -689,7 +689,7 @@ def test_config3_exact_sizes(oracle, n):
     assert ok, msg
 
 
-def _config4_bucket(oracle, dtype, per_input):
+def _config4_bucket(oracle, dtype, per_input, each=False):
     """Config 4: n = 8, `per_input` bytes per input split into 1 MiB computes
     with the partition() formula (reduce.h:401-415; pipedepth = bytes / 1 MiB,
     as SURVEY.md 8d C4), ONE batched plan launch; checked at a random sample,
@@ -711,7 +711,7 @@ def _config4_bucket(oracle, dtype, per_input):
         comp.add([(t, off) for t in ins], (out, off), c, compid=0)
         off += c
     assert off == count and comp.numcomp == depth
-    comp.start(stream=torch.cuda.current_stream())
+    comp.start(stream=torch.cuda.current_stream(), each=each)
     torch.cuda.synchronize()
     bounds = [b * (count // depth) + min(b, count % depth) for b in range(depth)]
     ok, msg = _sampled(out, n, count, seed, bf16=(dtype == torch.bfloat16),
@@ -727,6 +727,17 @@ def _config4_bucket(oracle, dtype, per_input):
 def test_config4_exact_256MiB_in_1MiB_computes(oracle, dtype):
     """Config 4 at 256 MiB per input: 256 computes of 1 MiB in one launch."""
     _config4_bucket(oracle, dtype, 256 << 20)
+
+
+@pytest.mark.parametrize("each", [False, True], ids=["batched", "launch_per_compute"])
+@pytest.mark.parametrize("per_input", [16 << 20, 64 << 20], ids=["16MiB", "64MiB"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_config4_small_in_1MiB_computes(oracle, dtype, per_input, each):
+    """Config 4's smallest sizes (16 and 64 computes of 1 MiB), both ways
+    SURVEY.md 8d reports them: one batched plan launch, and the reference's
+    structure of one launch per compute (compute.h:88-91;
+    hiccl_reduce_plan_launch_each)."""
+    _config4_bucket(oracle, dtype, per_input, each=each)
 
 
 @pytest.mark.parametrize("per_input", [1 << 30, 4 << 30], ids=["1GiB", "4GiB"])
