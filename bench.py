@@ -139,9 +139,10 @@ def c5_leg(args):
     return obj[0]
 
 
-def run_c5(world, args, allow_shared=False):
+def run_c5(world, args, allow_shared=False, only=None):
     """`allow_shared`: run even with fewer GPUs than ranks (a rehearsal on a
-    1-GPU box, tests/test_c5_leg_gpu.py; the library then runs host-driven)."""
+    1-GPU box, tests/test_c5_leg_gpu.py; the library then runs host-driven).
+    `only`: run just these mode keys."""
     import shutil
     import tempfile
     # the MPI ranks pick their GPU by local rank (CommBench::init); a per-rank
@@ -190,6 +191,8 @@ def run_c5(world, args, allow_shared=False):
     modes.append(("xccl", {"HICCL_STREAM_ORDERED": "0", "HICCL_XCCL": "rccl"}, hier, libs.replace("ipc", "xccl")))
     modes.append(("stream_graph_fused", dict(fenced, HICCL_STEP_PROGRAM="1", HICCL_PROG_FENCES="light"), hier, libs))
     deadline = time.perf_counter() + 300.0  # the whole leg: never more than ~5 min of the bench run
+    if only is not None:
+        modes = [m for m in modes if m[0] in only]
     for name, extra, hier, libs in modes:
         left = int(deadline - time.perf_counter())
         if left < 30:

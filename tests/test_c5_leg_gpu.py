@@ -44,3 +44,21 @@ def test_c5_leg_rehearsal_one_gpu(ranks):
     assert ab["baseline_kat"] == "PASSED" and ab["baseline_ms"] > 0
     for name in ("stream_graph_fused_fenced", "stream_graph_fused"):
         assert ab[name]["kat"] == "PASSED" and ab[name]["over_baseline"] > 0
+
+
+def test_config5_exact_shape_one_gpu():
+    """Config 5 at its exact shape and size (collectives/main.cpp:151-155 with
+    {1,4,2} {MPI,IPC,IPC}, 2^25 floats per rank per chunk = a 1 GiB send
+    buffer per rank, pipedepth 128) with all 8 ranks on the box's one GPU
+    (host-driven, the shared-device fallback): the all-reduce's float-exact
+    known-answer check passes at full size, every step's batched kernel is
+    timed.  Parity only -- one GPU moves the "xGMI" bytes through its own
+    HBM, so the times rank nothing."""
+    import bench
+    res = bench.run_c5(8, argparse.Namespace(c5_log2count=25, c5_iters=1), allow_shared=True, only=("host",))
+    r = res["host"]
+    assert r.get("kat") == "PASSED" and r["kat_exact_mismatches"] == 0, r
+    assert r["rc"] == 0 and r["ranks"] == 8 and r["hierarchy"] == "1,4,2" and r["libs"] == "MPI,IPC,IPC"
+    assert r["pipedepth"] == 128 and r["count_per_rank_chunk"] == 1 << 25
+    assert r["sendbuf_bytes_per_rank"] == float(8 << 27)  # 2^25 floats x 8 ranks x 4 B = 1 GiB
+    assert r["kernel_steps_rank0"] > 0 and r["kernel_ms_per_run_max_rank"] > 0
