@@ -192,3 +192,21 @@ def test_c5_driver_json_records_devices_and_mode(tmp_path):
         assert hs[k] >= 0.0, k
     assert hs["transport_wait"] + hs["compute_wait"] > 0.0
     assert hs["enqueue"] == 0.0 and hs["sync"] == 0.0
+
+
+def test_c5_protocol_ab_summary():
+    """protocol_ab: each program / light-token twin's median collective time
+    over the default protocol's (stream_graph_fused_noprog), with its KAT and
+    mode_used; a mode that did not run gives None, never a ratio."""
+    sys.path.insert(0, ROOT)
+    import bench
+    out = {"stream_graph_fused_noprog": {"collective_ms_median": 2.0, "kat": "PASSED"},
+           "stream_graph_fused_fenced": {"collective_ms_median": 1.5, "kat": "PASSED",
+                                         "mode_used": "stream-ordered+graph+fused+program+tokens-fenced"},
+           "stream_graph_fused": {"skipped": "time budget of the config-5 leg spent"}}
+    ab = bench.c5_protocol_ab(out)
+    assert ab["baseline_ms"] == 2.0 and ab["baseline_kat"] == "PASSED"
+    assert ab["stream_graph_fused_fenced"]["over_baseline"] == 0.75
+    assert ab["stream_graph_fused_fenced"]["mode_used"].endswith("tokens-fenced")
+    assert ab["stream_graph_fused"]["ms"] is None and ab["stream_graph_fused"]["over_baseline"] is None
+    assert bench.c5_protocol_ab({})["stream_graph_fused"]["over_baseline"] is None
