@@ -874,7 +874,7 @@ def c3_vs_c2(args):
         write = mix_ceiling(ins, out, count, mode=2)
         buckets.append({"config": cfg, "n": n, "count": count, "ins": ins, "out": out, "read": read, "write": write,
                         "ms": []})
-        log(f"c3vsc2: {cfg} n={n} allocated, probes read {read:.0f} write {write:.0f} GB/s")
+        log(f"c3vsc2: {cfg} n={n} allocated, probes read {read} write {write} GB/s")
     for rnd in range(args.rounds):
         for b in buckets:
             _, ms = time_launches(lambda: hiccl_amd.reduce(b["out"], b["ins"]), args.steps, args.warmup)

@@ -205,3 +205,15 @@ def test_stream_ordered_defaults_resolve_as_stated(monkeypatch):
     for v, want in (("1", 1), ("0", 0), ("", 0), ("yes", 0)):
         monkeypatch.setenv("HICCL_STEP_PROGRAM", v)
         assert lib.hiccl_step_program_default() == want, v
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No CPU fallback: with the HIP library absent every entry point raises
+    (the product never computes on the host instead)."""
+    import torch
+    monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "libhiccl_reduce.so"))
+    monkeypatch.setattr(L, "_lib", None)
+    with pytest.raises(ImportError, match="HIP extension missing"):
+        L.lib()
+    with pytest.raises(ImportError, match="HIP extension missing"):
+        hiccl_amd.Compute(torch.float32, device=0)
