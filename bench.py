@@ -1153,19 +1153,14 @@ def progstep(args):
         p_copy.launch([epoch[0]], err=err.data_ptr(), timeout_s=10.0, stream=stream)
         p_comp.launch([epoch[0]], err=err.data_ptr(), timeout_s=10.0, stream=stream)
 
-    def separate_full():  # the signal kernels with release stores, acquire polls and fences
-        os.environ["HICCL_PROG_FENCES"] = "full"
-        try:
-            separate()
-        finally:
-            os.environ.pop("HICCL_PROG_FENCES", None)
-
-    def program_tail_folded_full():  # the prologue with release stores and fences (HICCL_PROG_FENCES=full)
-        os.environ["HICCL_PROG_FENCES"] = "full"
-        try:
-            program_tail_folded()
-        finally:
-            os.environ.pop("HICCL_PROG_FENCES", None)
+    def tokens(mode, fn):  # run fn with the token protocol `mode` (HICCL_PROG_FENCES, read at each launch)
+        def run():
+            os.environ["HICCL_PROG_FENCES"] = mode
+            try:
+                fn()
+            finally:
+                os.environ.pop("HICCL_PROG_FENCES", None)
+        return run
 
     def separate_nophase():
         cp.enqueue(stream)
@@ -1177,9 +1172,11 @@ def progstep(args):
         q_copy.launch(stream=stream)
         q_comp.launch(stream=stream)
 
-    runs = {"separate": separate, "separate_full_fences": separate_full, "program": program,
+    # unsuffixed: the library's default token protocol (fenced); _light:
+    # HICCL_PROG_FENCES=light
+    runs = {"separate": separate, "separate_light": tokens("light", separate), "program": program,
             "program_tail_folded": program_tail_folded,
-            "program_tail_folded_full_fences": program_tail_folded_full,
+            "program_tail_folded_light": tokens("light", program_tail_folded),
             "separate_no_phases": separate_nophase, "program_no_phases": program_nophase}
     res = {k: [] for k in runs}
     for _ in range(5):
@@ -1199,10 +1196,10 @@ def progstep(args):
 
     side = torch.cuda.Stream()
     graphs = {}
-    for name in ("separate_graph", "program_tail_folded_graph", "program_tail_folded_full_fences_graph",
-                 "separate_no_phases_graph", "program_no_phases_graph"):
-        if name == "program_tail_folded_full_fences_graph":
-            os.environ["HICCL_PROG_FENCES"] = "full"  # read at each launch: the capture keeps it
+    for name in ("separate_graph", "separate_light_graph", "program_tail_folded_graph",
+                 "program_tail_folded_light_graph", "separate_no_phases_graph", "program_no_phases_graph"):
+        if "_light" in name:
+            os.environ["HICCL_PROG_FENCES"] = "light"  # read at each launch: the capture keeps it
         g = torch.cuda.CUDAGraph()
         with torch.cuda.stream(side):
             cs = torch.cuda.current_stream()
@@ -1211,13 +1208,13 @@ def progstep(args):
                 L.check(lib.hiccl_counter_add(cptr, 1, s_), "counter_add")
                 for i in range(200):
                     e = 1000 + i
-                    if name == "separate_graph":
+                    if name in ("separate_graph", "separate_light_graph"):
                         phase_dev(f[0], e, s_)
                         cp.enqueue(cs)
                         phase_dev(f[1], e, s_)
                         comp.enqueue(cs)
                         phase_dev(f[2], e, s_)
-                    elif name in ("program_tail_folded_graph", "program_tail_folded_full_fences_graph"):
+                    elif name in ("program_tail_folded_graph", "program_tail_folded_light_graph"):
                         p_copy.launch([e], epoch_dev=ctr.data_ptr(), err=err.data_ptr(), timeout_s=10.0, stream=cs)
                         p_comp.launch([e], epoch_dev=ctr.data_ptr(), err=err.data_ptr(), timeout_s=10.0, stream=cs)
                     elif name == "separate_no_phases_graph":
@@ -1252,7 +1249,8 @@ def progstep(args):
     torch.cuda.synchronize()
     mib = 1 << 20
     alg = (12 + 5) * mib + (5 + 5) * mib  # reductions: 12 MiB read + 5 written; copies: 5 MiB read + 5 written
-    row = {"mode": "progstep", "err": int(err.item()), "bits_ok": bool(ok), "algorithmic_bytes": alg}
+    row = {"mode": "progstep", "err": int(err.item()), "bits_ok": bool(ok), "algorithmic_bytes": alg,
+           "default_tokens": "fenced" if lib.hiccl_token_mode() == L.HICCL_TOKENS_FENCED else "light"}
     for k, v in res.items():
         row[k + "_us"] = round(float(np.median(v)), 3)
     row["saved_us_per_step"] = round(row["separate_us"] - row["program_us"], 3)

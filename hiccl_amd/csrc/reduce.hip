@@ -701,8 +701,8 @@ constexpr int kMaxFlags = 64;  // signal and wait flags per launch (one per lane
 
 // Several signal/wait phases in ONE launch, executed in order: phase p
 // stores its epoch to its flags (system-scope release), then waits for its
-// flags (system-scope acquire); phase p + 1 starts after every wait of phase
-// p has finished.  The transport queues the consecutive signal/wait steps of
+// flags (relaxed polls, then a system-scope acquire fence); phase
+// p + 1 starts after every wait of phase p has finished.  The transport queues the consecutive signal/wait steps of
 // a stream-ordered pipeline (a step's done tokens, the next step's readies)
 // into one such launch instead of one launch each: same order of every
 // operation on the stream, fewer kernel boundaries (~1.5-1.9 us each).
@@ -737,10 +737,12 @@ __global__ __launch_bounds__(64) void k_sigwait_phases(SigPhaseArgs a) {
     if (w0 + lane < w1) {
       const uint32_t *f = a.wait[w0 + lane];
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      auto poll = [&]() {
-        return a.light ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                       : __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-      };
+      // relaxed polls in both modes (no cache invalidate per poll); in the
+      // fenced mode the system-scope acquire fence below, executed by
+      // this lane after its last poll, makes the load that saw the peer's
+      // release store synchronise with it -- the fence form of an acquire
+      // load, paid once per phase instead of once per poll
+      auto poll = [&]() { return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
       while ((int32_t)(poll() - epoch) < 0) {
         __builtin_amdgcn_s_sleep(2);
         if (a.err && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
@@ -750,9 +752,12 @@ __global__ __launch_bounds__(64) void k_sigwait_phases(SigPhaseArgs a) {
         }
       }
     }
-    // every lane's waits of this phase precede any store of the next one
+    // fenced mode: each lane's acquire half of its polls, sequenced after
+    // its last poll; then every lane's waits (and acquires, carried to the
+    // other lanes by the barrier's workgroup-scope fences) precede any store
+    // of the next phase
+    if (!a.light) __atomic_thread_fence(__ATOMIC_ACQUIRE);
     __syncthreads();
-    if (!a.light) __atomic_thread_fence(__ATOMIC_ACQ_REL);
     s0 = s1;
     w0 = w1;
   }
@@ -831,9 +836,10 @@ struct ProgArgs {
 // after the gate, on workgroups whose L1 holds none of their data (the
 // kernel-start acquire invalidated it and nothing read it since).  The wave
 // issues a phase's stores only after its polls of the previous phase have
-// returned (the loop exits on the loaded value).  Fenced mode (the default:
-// release stores, an acquire-release fence per phase, a release gate store)
-// relies on the memory model alone.
+// returned (the loop exits on the loaded value).  Fenced mode (the
+// default: release stores, an acquire fence per phase after relaxed polls, a
+// release gate store and an acquire fence after each gate wait) relies on
+// the memory model alone.
 __device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t count, uint32_t lane, uint32_t add) {
   for (uint32_t p = 0; p < count; p++) {
     const ConstU32 *q = (const ConstU32 *)&a.phase[p];
@@ -859,9 +865,15 @@ __device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t count, u
         }
       }
     }
-    // every lane's waits of this phase precede any store of the next one
+    // fenced mode: each lane's acquire half of its polls, after its last
+    // poll; then every lane's waits (and acquires) precede any store of the
+    // next phase -- a wave-level barrier whose wavefront-scope fences carry
+    // the ordering from lane to lane (only this wave runs the phases, so no
+    // workgroup barrier is available here)
+    if (!a.light) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (!a.light) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -935,6 +947,10 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
       }
     } else if (tid == 0) {
       prog_gate_wait(a, seq);
+      // fenced mode: the acquire half of the gate poll, so the units below
+      // are ordered after workgroup 0's phases (its release gate store);
+      // the barrier carries it to the workgroup's other threads
+      if (a.light == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
   }
@@ -954,7 +970,7 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
 // ------------------------------------------------------------ host side ----
 
 // Token protocol of programs and of k_sigwait_phases (hiccl_token_mode).
-// Default FENCED: release token stores, acquire polls / an acquire-release
+// Default FENCED: release token stores, relaxed polls then an acquire
 // fence per phase, a release gate store -- the memory model's own guarantee.
 // HICCL_PROG_FENCES=light: relaxed stores and polls, no fences (prog_phases'
 // argument rests on kernel-boundary cache behaviour that only a run with one

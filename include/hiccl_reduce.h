@@ -370,8 +370,9 @@ void hiccl_program_destroy(hiccl_program_t *prog);
  * call (launches resolve them the same way; no device needed).
  *   hiccl_token_mode: the token phases of hiccl_signal_wait* and programs.
  *     HICCL_TOKENS_FENCED (default; HICCL_PROG_FENCES unset, "full" or any
- *     other value): system-scope release token stores, acquire polls, an
- *     acquire-release fence per phase, a release gate store -- ordering by the
+ *     other value): system-scope release token stores, relaxed polls closed
+ *     by a system-scope acquire fence per phase (the fence form of an
+ *     acquire load), a release gate store -- ordering by the
  *     memory model alone.  HICCL_TOKENS_LIGHT (HICCL_PROG_FENCES=light):
  *     relaxed stores and polls, no fences; 0.4-4.5 us cheaper per step on one
  *     GPU, but its argument (tokens publish nothing of their own launch) leans
