@@ -838,8 +838,9 @@ struct ProgArgs {
 // issues a phase's stores only after its polls of the previous phase have
 // returned (the loop exits on the loaded value).  Fenced mode (the
 // default: release stores, an acquire fence per phase after relaxed polls, a
-// release gate store and an acquire fence after each gate wait) relies on
-// the memory model alone.
+// release gate store) orders workgroup 0 after the peers by the memory model;
+// the gate hand-off to the other workgroups is relaxed in both modes (see
+// k_program).
 __device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t count, uint32_t lane, uint32_t add) {
   for (uint32_t p = 0; p < count; p++) {
     const ConstU32 *q = (const ConstU32 *)&a.phase[p];
@@ -946,11 +947,14 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
         }
       }
     } else if (tid == 0) {
+      // Relaxed in both modes: no unit of this launch touches its data before
+      // the gate opens, and the kernel-start acquire left no line of it in
+      // this CU's L1 or this XCD's L2.  A system-scope acquire here, one per
+      // workgroup (1,024 L2 invalidations per launch), cost ~8 us per C5 step
+      // (profiles/r04f_progstep.jsonl: program_tail_folded 20.8 / 19.4 us
+      // eager / graph vs 13.2 / 10.9 light); the per-element launches, the
+      // default, hand off at real kernel boundaries instead.
       prog_gate_wait(a, seq);
-      // fenced mode: the acquire half of the gate poll, so the units below
-      // are ordered after workgroup 0's phases (its release gate store);
-      // the barrier carries it to the workgroup's other threads
-      if (a.light == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
   }

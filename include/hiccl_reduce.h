@@ -372,12 +372,14 @@ void hiccl_program_destroy(hiccl_program_t *prog);
  *     HICCL_TOKENS_FENCED (default; HICCL_PROG_FENCES unset, "full" or any
  *     other value): system-scope release token stores, relaxed polls closed
  *     by a system-scope acquire fence per phase (the fence form of an
- *     acquire load), a release gate store -- ordering by the
- *     memory model alone.  HICCL_TOKENS_LIGHT (HICCL_PROG_FENCES=light):
- *     relaxed stores and polls, no fences; 0.4-4.5 us cheaper per step on one
- *     GPU, but its argument (tokens publish nothing of their own launch) leans
- *     on kernel-boundary cache behaviour across GPUs that no run with one GPU
- *     per rank has confirmed yet, so it is opt-in.
+ *     acquire load), a release gate store -- every token ordered by the
+ *     memory model (a program's gate hand-off to its own other workgroups
+ *     stays relaxed in both modes).  HICCL_TOKENS_LIGHT
+ *     (HICCL_PROG_FENCES=light): relaxed stores and polls, no fences; the
+ *     same cost for per-element launches, ~8 us per step cheaper for
+ *     programs on one GPU, but its argument (tokens publish nothing of their
+ *     own launch) leans on kernel-boundary cache behaviour across GPUs that
+ *     no run with one GPU per rank has confirmed yet, so it is opt-in.
  *   hiccl_step_program_default: 1 when HiCCL::Comm's stream-ordered mode folds
  *     token phases into step programs (HICCL_STEP_PROGRAM=1), else 0 -- one
  *     launch per element, the protocol the GPU suite verifies by default. */
