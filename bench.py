@@ -972,6 +972,15 @@ def schedsweep(args):
                     ("tile_static", dict(engine=1, schedule=1)),
                     ("phase_static", dict(engine=2, schedule=1)),
                     ("phase_dyn", dict(engine=2, schedule=2))]
+    if args.sweepset == "fewn":  # config 3's few-input buckets (n = 2-4): every engine form, interleaved
+        variants = [("auto", None),
+                    ("phase_static", dict(engine=2, schedule=1)),
+                    ("phase_dyn", dict(engine=2, schedule=2)),
+                    ("tile_u4_static", dict(engine=1, schedule=1)),
+                    ("tile_u4_dyn", dict(engine=1, schedule=2)),
+                    ("tile_u8_static", dict(engine=1, unroll=8, schedule=1)),
+                    ("tile_u8_dyn", dict(engine=1, unroll=8, schedule=2, grab=1)),
+                    ("tile_u4_static_bpc2", dict(engine=1, schedule=1, blocks_per_cu=2))]
     if args.sweepset == "xover":  # engine x schedule crossover (sets AUTO)
         variants = [("auto", None),
                     ("tile_dyn", dict(engine=1, schedule=2)),
