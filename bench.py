@@ -590,6 +590,7 @@ def main():
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--nway", action="store_true")
     ap.add_argument("--c3vsc2", action="store_true", help="C3 per n interleaved with C2 on one box")
+    ap.add_argument("--c3offsets", action="store_true", help="C3 few inputs: relative input placement")
     ap.add_argument("--rounds", type=int, default=5, help="c3vsc2: interleaved rounds")
     ap.add_argument("--chunks", action="store_true")
     ap.add_argument("--roundtrip", action="store_true")
@@ -635,6 +636,8 @@ def main():
         return nway(args)
     if args.c3vsc2:
         return c3_vs_c2(args)
+    if args.c3offsets:
+        return c3_offsets(args)
     if args.chunks:
         return chunks(args)
     if args.c2variants:
@@ -905,6 +908,46 @@ def c3_vs_c2(args):
                       "c3_ratio_to_c2": {r["n"]: r["ratio_to_c2"] for r in c3},
                       "c3_model_frac": {r["n"]: (r["serial_rw_model"] or {}).get("frac_write_probe") for r in c3},
                       "device": torch.cuda.get_device_properties(0).name}), flush=True)
+    return 0
+
+
+def c3_offsets(args):
+    """Config 3 with few inputs: does where the inputs sit relative to each
+    other move the rate?  n in {2, 3, 4, 8} x 2^26 fp32; input k is a view
+    starting k x `off` bytes into a padded allocation (off = 0, 4 KiB,
+    64 KiB, 1 MiB + 4 KiB), so element i of every input no longer shares its
+    address bits below the offset with the other inputs; AUTO and every
+    engine form that leads somewhere, interleaved rounds, one set of
+    allocations per n (the same physical pages for every offset)."""
+    count = 1 << 26
+    offs = (0, 4 << 10, 64 << 10, (1 << 20) + (4 << 10))
+    forms = [("auto", None), ("phase", dict(engine=2, schedule=1)), ("tile_u4_static", dict(engine=1, schedule=1))]
+    for n in (2, 3, 4, 8):
+        pad = (n - 1) * max(offs) // 4 + 64
+        raw = [torch.empty(count + pad, device="cuda") for _ in range(n)]
+        out = torch.empty(count, device="cuda")
+        res = {}
+        for rnd in range(args.rounds):
+            for off in offs:
+                ins = [raw[k][k * off // 4:k * off // 4 + count] for k in range(n)]
+                if rnd == 0:
+                    for k, t in enumerate(ins):
+                        hiccl_amd.fill_uniform(t, SEED + off, k)
+                for name, cfg in forms:
+                    _, ms = time_launches(lambda: hiccl_amd.reduce(out, ins, config=cfg), args.steps, args.warmup)
+                    res.setdefault((off, name), []).append(float(np.median(ms)))
+                if rnd == 0:
+                    torch.cuda.synchronize()
+                    res[(off, "ok")] = sample_check(out, n, count, seed=SEED + off)
+        alg = (n + 1) * count * 4
+        row = {"mode": "c3offsets", "n": n, "count": count}
+        for off in offs:
+            row[f"off{off}"] = {name: round(alg / (float(np.median(res[(off, name)])) * 1e-3) / 1e9, 1)
+                                for name, _ in forms}
+            row[f"off{off}"]["sample_exact"] = res[(off, "ok")]
+        print(json.dumps(row), flush=True)
+        del raw, out
+        torch.cuda.empty_cache()
     return 0
 
 
