@@ -188,6 +188,16 @@ inline bool xccl_rccl_requested() {
   const char *e = std::getenv("HICCL_XCCL");
   return e && std::string(e) == "rccl";
 }
+// HICCL_XCCL_SELF=rccl (test knob): a rank's self transfers of an XCCL level
+// go through RCCL too (ncclSend / ncclRecv to itself in the step's group)
+// instead of the batched copy kernel -- so a one-rank job on one GPU runs
+// the RCCL path end to end (communicator, groups, destroy) and the KAT
+// checks the bytes RCCL moved.  RCCL refuses two ranks on one GPU, so this
+// is the only form of the path a single-GPU box can execute.
+inline bool xccl_self_on_rccl() {
+  const char *e = std::getenv("HICCL_XCCL_SELF");
+  return e && std::string(e) == "rccl";
+}
 
 // Communicators whose XCCL levels run on RCCL; the last one to go destroys
 // the RCCL communicator (xccl_release), so ncclCommDestroy runs before
@@ -1234,6 +1244,7 @@ class Comm {
     if (lib == dummy) return;
     for (const Xfer &x : xfers) {
       if (!x.count) continue;
+      if (lib == XCCL && xccl_self_on_rccl()) continue;  // every transfer of the level is RCCL's (xccl_group)
       const bool self = x.sendid == x.recvid && x.sendid == myid;
       const bool move = x.sendid != x.recvid && !x.fused && (lib == IPC || lib == IPC_get) && myid == mover_of(x);
       if (!self && !move) continue;
@@ -1280,13 +1291,16 @@ class Comm {
     build_plans();
     if (selfplan) launch_plan(selfplan, s, "self copies");
 #ifdef HICCL_WITH_RCCL
+    const bool self_too = xccl_self_on_rccl();
+    auto on_rccl = [&](const Xfer &x) {
+      return x.count && (x.sendid != x.recvid || self_too) && (myid == x.sendid || myid == x.recvid);
+    };
     bool any = false;
-    for (const Xfer &x : xfers)
-      if (x.count && x.sendid != x.recvid && (myid == x.sendid || myid == x.recvid)) any = true;
+    for (const Xfer &x : xfers) any = any || on_rccl(x);
     if (!any) return;
     nccl_check(ncclGroupStart(), "ncclGroupStart");
     for (const Xfer &x : xfers) {
-      if (!x.count || x.sendid == x.recvid) continue;
+      if (!on_rccl(x)) continue;
       if (myid == x.sendid)
         nccl_check(ncclSend(x.src, x.count * sizeof(T), ncclUint8, x.recvid, xccl_comm(), s), "ncclSend");
       if (myid == x.recvid)

@@ -271,3 +271,21 @@ def test_xccl_level_on_rccl(streamed):
                      stream_env="1" if streamed else "0", extra_env={"HICCL_XCCL": "rccl"})
     assert rc == 0, out[-3000:]
     assert "PASSED!" in out and "XCCL on RCCL" in out
+
+
+@pytest.mark.parametrize("streamed", [False, True], ids=["host", "stream"])
+@pytest.mark.parametrize("pattern", [8, 6, 4])
+def test_xccl_level_on_rccl_single_rank(pattern, streamed):
+    """The form of the RCCL path one GPU can run (RCCL refuses two ranks on
+    one device): ONE rank whose XCCL level's self transfers go through RCCL
+    (HICCL_XCCL_SELF=rccl) -- the communicator from an MPI-broadcast id, one
+    ncclGroupStart / ncclSend / ncclRecv / ncclGroupEnd per step on the
+    transport stream, host-driven and stream-ordered, destroyed with the last
+    communicator; the reference's known-answer test checks the bytes RCCL
+    moved.  Cross-GPU RCCL (test_xccl_level_on_rccl) needs >= 2 GPUs."""
+    rc, out = mpirun(1, HIP, [pattern, 4099, 1, 1, 3, 0, 0, "1", "xccl"], streamed=streamed,
+                     stream_env="1" if streamed else "0",
+                     extra_env={"HICCL_XCCL": "rccl", "HICCL_XCCL_SELF": "rccl"})
+    assert rc == 0, out[-3000:]
+    assert "PASSED!" in out and "XCCL on RCCL" in out, out[-3000:]
+    assert ("stream-ordered" if streamed else "host-driven") in out
