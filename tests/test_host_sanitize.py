@@ -66,3 +66,20 @@ def test_plan_dump_clean_and_identical(args):
     plain = subprocess.run([os.path.join(ROOT, "build", "plan_dump")] + args, capture_output=True, text=True,
                            check=True).stdout
     assert san == plain
+
+
+def test_driver_json_and_step_timing_clean(tmp_path):
+    """bench.py's config-5 JSON path (HICCL_DRIVER_JSON: HiCCL::measure, the
+    known-answer run, Comm::set_step_timing's timed runs) under the
+    sanitizers, on config 5's hierarchy."""
+    import json
+    path = tmp_path / "c5.json"
+    cmd = [MPIRUN, "-np", "8", os.path.join(SAN, "collectives_host_f32"), "8", "1000", "1", "1", "3", "1", "2",
+           "1,4,2", "mpi,ipc,ipc"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=dict(ENV, HICCL_DRIVER_JSON=str(path)),
+                       cwd="/tmp")
+    out = p.stdout + p.stderr
+    assert "Sanitizer" not in out and "runtime error" not in out, out[-3000:]
+    assert p.returncode == 0, out[-3000:]
+    r = json.loads(path.read_text())
+    assert r["kat"] == "PASSED" and r["host_split_us_per_step"]["runs"] == 2
