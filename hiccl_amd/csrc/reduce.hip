@@ -25,7 +25,11 @@
 //    gfx950 serves unaligned dwordx4 loads in hardware;
 //  * a batched plan kernel runs every compute of a pipeline step in ONE launch
 //    from a device descriptor table (vs one kernel + one stream + one
-//    hipStreamSynchronize per compute, compute.h:87-117).
+//    hipStreamSynchronize per compute, compute.h:87-117);
+//  * stream-ordered transport signalling (k_sigwait_phases) and step
+//    programs (k_program: token phases folded into a batch's launch), with
+//    fenced tokens by default (release stores, relaxed polls closed by one
+//    acquire fence per phase; hiccl_token_mode).
 //
 // Layout / roofline / measured numbers: DESIGN.md.
 
