@@ -1024,6 +1024,14 @@ def schedsweep(args):
                     ("tile_u8_static", dict(engine=1, unroll=8, schedule=1)),
                     ("tile_u8_dyn", dict(engine=1, unroll=8, schedule=2, grab=1)),
                     ("tile_u4_static_bpc2", dict(engine=1, schedule=1, blocks_per_cu=2))]
+    if args.sweepset == "phaseshapes":  # the phased engine's chunk shapes (block x packets per lane)
+        variants = [("auto", None),
+                    ("p512x16", dict(engine=2, block=512, unroll=16)),
+                    ("p1024x8", dict(engine=2, block=1024, unroll=8)),
+                    ("p512x8", dict(engine=2, block=512, unroll=8)),
+                    ("p1024x4", dict(engine=2, block=1024, unroll=4)),
+                    ("p256x16", dict(engine=2, block=256, unroll=16)),
+                    ("p256x16_bpc2", dict(engine=2, block=256, unroll=16, blocks_per_cu=2))]
     if args.sweepset == "xover":  # engine x schedule crossover (sets AUTO)
         variants = [("auto", None),
                     ("tile_dyn", dict(engine=1, schedule=2)),
