@@ -7,7 +7,11 @@ dispatch (median): FETCH_SIZE x 2 + WRITE_SIZE = HBM bytes (the gfx950
 corrections of MI355X_MICROARCH.md's HBM section: FETCH_SIZE counts half of a
 16-B/lane streaming read; both in KiB), SQ_* wave/instruction counts.
 
-    python tools/plan_pmc_summary.py <tag>
+    python tools/plan_pmc_summary.py <tag> [shape-label algorithmic-bytes]
+
+The optional pair names the shape of every launch of a single-shape run
+(tools/plan_shapes.py --shapes d), whose grid the table below cannot tell
+from shape b's.
 """
 import csv
 import glob
@@ -58,6 +62,8 @@ def main():
     for key, ds in durs.items():
         name, grid = key
         shape, alg = SHAPES.get(grid, ("?", None))
+        if len(sys.argv) > 3:
+            shape, alg = sys.argv[2], int(sys.argv[3])
         c = {k: st.median(v) for k, v in counters.get(key, {}).items()}
         rec = {"kernel": name, "grid_threads": grid, "shape": shape, "dispatches": len(ds),
                "duration_us_median": round(st.median(ds), 3), "duration_us_min": round(min(ds), 3),

@@ -4,6 +4,9 @@
   (a) C4 at 16 MiB per input: n = 8, 16 computes of 1 MiB, f32 and bf16
   (b) C4 bf16 at 1 GiB per input: n = 8, 1024 computes of 1 MiB, against the
       one-shot launch of the same bucket (interleaved)
+  (d) C4 f32 at 4 GiB per input: n = 8, 4096 computes of 1 MiB (byte
+      offsets past 2^32 inside one batched plan), against the one-shot
+      launch of the same bucket (interleaved)
   (c) a C5-shaped step: four n = 2 and one n = 4 computes of 2^18 f32
       (collectives/main.cpp:151-155 with {1,4,2}, 1 GiB per rank,
       pipedepth 128: reduce.h:134-170 emission per batch)
@@ -188,6 +191,28 @@ def main():
                           "parity_sample_ok": bench.sample_check(out, 8, count, bf16=True)}), flush=True)
         for _, c in vs:
             c.close()
+        del ins, out
+        torch.cuda.empty_cache()
+    if "d" in shapes:
+        count = 4096 * MIB // 4
+        comp, ins, out = partitioned_plan(torch.float32, 8, count, 4096)
+        nbytes = 9 * count * 4
+        res = {}
+        for _ in range(args.rounds):
+            _, ms = bench.time_launches(lambda: comp.start(stream=stream), args.steps, args.warmup)
+            res.setdefault("plan_4096", []).append(float(np.median(ms)))
+            _, ms = bench.time_launches(lambda: hiccl_amd.reduce(out, ins), args.steps, args.warmup)
+            res.setdefault("oneshot", []).append(float(np.median(ms)))
+        comp.start(stream=stream)
+        torch.cuda.synchronize()
+        for vname, v in res.items():
+            t = float(np.median(v))
+            print(json.dumps({"shape": "d_C4_f32_4GiB_x4096", "variant": vname,
+                              "engine": comp.engine() if vname.startswith("plan") else None,
+                              "event_us": round(t * 1e3, 1), "event_GBps": round(nbytes / t / 1e6, 1)}), flush=True)
+        print(json.dumps({"shape": "d_C4_f32_4GiB_x4096",
+                          "parity_sample_ok": bench.sample_check(out, 8, count)}), flush=True)
+        comp.close()
         del ins, out
         torch.cuda.empty_cache()
     if "c" in shapes:

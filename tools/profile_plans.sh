@@ -4,14 +4,14 @@
 # 1 GiB, a C5-shaped step).  One --kernel-trace --stats pass, then counters in
 # separate --pmc passes (never combined with tracing; <= 4 TCC per pass:
 # FETCH_SIZE and WRITE_SIZE apart), per MI355X_MICROARCH.md's recipe.
-#   usage (on the GPU box): tools/profile_plans.sh <tag>
+#   usage (on the GPU box): tools/profile_plans.sh <tag> [shapes, default a,b,c]
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=$1
 out=gpurun_out/prof_$tag
 rm -rf "$out"; mkdir -p "$out"
-run="python3 tools/plan_shapes.py --steps 10 --warmup 3 --rounds 1"
+run="python3 tools/plan_shapes.py --steps 10 --warmup 3 --rounds 1 --shapes ${2:-a,b,c}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o run -- \
   $run > "$out/stats.log" 2>&1
 i=0
