@@ -129,8 +129,12 @@ static int bench_json(const char *path, HiCCL::Comm<Type> &coll, Type *sendbuf_d
   // start / wait, compute launch / wait in comm.h:195-204's order, or the
   // stream-ordered enqueue and final sync), microseconds per step, MAX over
   // ranks of each part
+  // (HICCL_HOST_SPLIT_RUNS extra runs, default 1, 0: none -- never numiter
+  // more full collectives inside a bench leg's time budget)
+  int split_runs = 1;
+  if (const char *e = std::getenv("HICCL_HOST_SPLIT_RUNS")) split_runs = std::max(0, std::atoi(e));
   coll.set_step_timing(true);
-  for (int r = 0; r < std::max(numiter, 1); r++) {
+  for (int r = 0; r < split_runs; r++) {
     MPI_Barrier(CommBench::comm_mpi);
     coll.run();
   }

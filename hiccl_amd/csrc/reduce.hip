@@ -39,6 +39,8 @@
 #include <string.h>
 
 #include <atomic>
+#include <cctype>
+#include <cstdio>
 #include <map>
 #include <mutex>
 #include <string>
@@ -842,9 +844,9 @@ struct ProgArgs {
 // issues a phase's stores only after its polls of the previous phase have
 // returned (the loop exits on the loaded value).  Fenced mode (the
 // default: release stores, an acquire fence per phase after relaxed polls, a
-// release gate store) orders workgroup 0 after the peers by the memory model;
-// the gate hand-off to the other workgroups is relaxed in both modes (see
-// k_program).
+// release gate store) orders workgroup 0 after the peers by the memory model,
+// and the other workgroups after workgroup 0 by an agent-scope acquire after
+// their gate polls (k_program); light mode leaves the gate hand-off relaxed.
 __device__ __forceinline__ void prog_phases(const ProgArgs &a, uint32_t count, uint32_t lane, uint32_t add) {
   for (uint32_t p = 0; p < count; p++) {
     const ConstU32 *q = (const ConstU32 *)&a.phase[p];
@@ -951,14 +953,18 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
         }
       }
     } else if (tid == 0) {
-      // Relaxed in both modes: no unit of this launch touches its data before
-      // the gate opens, and the kernel-start acquire left no line of it in
-      // this CU's L1 or this XCD's L2.  A system-scope acquire here, one per
-      // workgroup (1,024 L2 invalidations per launch), cost ~8 us per C5 step
-      // (profiles/r04f_progstep.jsonl: program_tail_folded 20.8 / 19.4 us
-      // eager / graph vs 13.2 / 10.9 light); the per-element launches, the
-      // default, hand off at real kernel boundaries instead.
       prog_gate_wait(a, seq);
+      // Fenced mode: an agent-scope acquire closes the relaxed gate polls,
+      // pairing with workgroup 0's agent-scope release store of the gate.
+      // Workgroup 0 acquired the peers' tokens at system scope before that
+      // release, so by transitivity every peer write a token covers happens
+      // before this workgroup's units (the memory model's guarantee, not
+      // the kernel-boundary cache argument `light` rests on).  Agent scope,
+      // not system: both ends of this hand-off run on this GPU; a
+      // system-scope acquire per workgroup (1,024 L2 invalidations per
+      // launch) cost ~8 us per C5 step (profiles/r04f_progstep.jsonl).
+      // The workgroup barrier below carries it to the other lanes.
+      if (!a.light) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
   }
@@ -979,7 +985,8 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
 
 // Token protocol of programs and of k_sigwait_phases (hiccl_token_mode).
 // Default FENCED: release token stores, relaxed polls then an acquire
-// fence per phase, a release gate store -- the memory model's own guarantee.
+// fence per phase, a release gate store and an agent-scope acquire after
+// each workgroup's gate polls -- the memory model's own guarantee.
 // HICCL_PROG_FENCES=light: relaxed stores and polls, no fences (prog_phases'
 // argument rests on kernel-boundary cache behaviour that only a run with one
 // GPU per rank can confirm, so it is opt-in until one has).  Read at every
@@ -2510,9 +2517,23 @@ void hiccl_program_destroy(hiccl_program_t *p) {
 
 int hiccl_token_mode(void) { return prog_light() ? HICCL_TOKENS_LIGHT : HICCL_TOKENS_FENCED; }
 
+// "1" / yes / on / true (any case) opt in; "0" / no / off / false / unset
+// keep the default (off).  Round 3 read any value but "0" as on: a value
+// that is neither spelling is read as off and named once on stderr, so a job
+// script's protocol never changes without a word.
 int hiccl_step_program_default(void) {
   const char *e = std::getenv("HICCL_STEP_PROGRAM");
-  return e && std::string(e) == "1";
+  if (!e) return 0;
+  std::string v(e);
+  for (auto &ch : v) ch = (char)std::tolower((unsigned char)ch);
+  if (v == "1" || v == "yes" || v == "on" || v == "true") return 1;
+  if (!(v.empty() || v == "0" || v == "no" || v == "off" || v == "false")) {
+    static std::atomic<bool> warned{false};
+    if (!warned.exchange(true))
+      std::fprintf(stderr, "HiCCL: HICCL_STEP_PROGRAM=%s not recognised (1/yes/on/true or 0/no/off/false); "
+                           "step programs stay off\n", e);
+  }
+  return 0;
 }
 
 // ---------------------------------------------------------- measurement --

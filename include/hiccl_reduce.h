@@ -372,17 +372,20 @@ void hiccl_program_destroy(hiccl_program_t *prog);
  *     HICCL_TOKENS_FENCED (default; HICCL_PROG_FENCES unset, "full" or any
  *     other value): system-scope release token stores, relaxed polls closed
  *     by a system-scope acquire fence per phase (the fence form of an
- *     acquire load), a release gate store -- every token ordered by the
- *     memory model (a program's gate hand-off to its own other workgroups
- *     stays relaxed in both modes).  HICCL_TOKENS_LIGHT
- *     (HICCL_PROG_FENCES=light): relaxed stores and polls, no fences; the
- *     same cost for per-element launches, ~8 us per step cheaper for
- *     programs on one GPU, but its argument (tokens publish nothing of their
- *     own launch) leans on kernel-boundary cache behaviour across GPUs that
- *     no run with one GPU per rank has confirmed yet, so it is opt-in.
+ *     acquire load), a release gate store, and in a program's other
+ *     workgroups an agent-scope acquire fence after their gate polls --
+ *     every token and the gate hand-off ordered by the memory model.
+ *     HICCL_TOKENS_LIGHT (HICCL_PROG_FENCES=light): relaxed stores and
+ *     polls, no fences; the same cost for per-element launches, cheaper for
+ *     programs on one GPU, but its argument (tokens
+ *     publish nothing of their own launch) leans on kernel-boundary cache
+ *     behaviour across GPUs that no run with one GPU per rank has confirmed
+ *     yet, so it is opt-in.
  *   hiccl_step_program_default: 1 when HiCCL::Comm's stream-ordered mode folds
- *     token phases into step programs (HICCL_STEP_PROGRAM=1), else 0 -- one
- *     launch per element, the protocol the GPU suite verifies by default. */
+ *     token phases into step programs (HICCL_STEP_PROGRAM=1, yes, on or true,
+ *     any case), else 0 -- one launch per element, the protocol the GPU
+ *     suite verifies by default; an unrecognised value reads as 0 and is
+ *     named once on stderr. */
 #define HICCL_TOKENS_FENCED 0
 #define HICCL_TOKENS_LIGHT 1
 int hiccl_token_mode(void);

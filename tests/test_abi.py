@@ -202,7 +202,9 @@ def test_stream_ordered_defaults_resolve_as_stated(monkeypatch):
                     ("LIGHT", L.HICCL_TOKENS_FENCED), ("0", L.HICCL_TOKENS_FENCED)):
         monkeypatch.setenv("HICCL_PROG_FENCES", v)
         assert lib.hiccl_token_mode() == want, v
-    for v, want in (("1", 1), ("0", 0), ("", 0), ("yes", 0)):
+    # round 3's truthy spellings keep working; anything else reads as off
+    for v, want in (("1", 1), ("0", 0), ("", 0), ("yes", 1), ("ON", 1), ("True", 1), ("off", 0), ("no", 0),
+                    ("2", 0), ("bogus", 0)):
         monkeypatch.setenv("HICCL_STEP_PROGRAM", v)
         assert lib.hiccl_step_program_default() == want, v
 

@@ -187,7 +187,7 @@ def test_c5_driver_json_records_devices_and_mode(tmp_path):
     # transport start / wait, compute launch / wait; the stream-ordered
     # parts stay 0 here), MAX over ranks
     hs = r["host_split_us_per_step"]
-    assert hs["steps"] >= 4 and hs["runs"] == 2 and hs["over_ranks"] == "max"
+    assert hs["steps"] >= 4 and hs["runs"] == 1 and hs["over_ranks"] == "max"
     for k in ("transport_start", "transport_wait", "compute_launch", "compute_wait", "finish"):
         assert hs[k] >= 0.0, k
     assert hs["transport_wait"] + hs["compute_wait"] > 0.0
@@ -210,3 +210,117 @@ def test_c5_protocol_ab_summary():
     assert ab["stream_graph_fused_fenced"]["mode_used"].endswith("tokens-fenced")
     assert ab["stream_graph_fused"]["ms"] is None and ab["stream_graph_fused"]["over_baseline"] is None
     assert bench.c5_protocol_ab({})["stream_graph_fused"]["over_baseline"] is None
+
+
+STUB_MPIRUN = r'''
+import json, os, sys
+# a stand-in for mpirun: behaviour per call from STUB_PLAN (a comma list),
+# the call number kept in STUB_COUNTER
+ctr = os.environ["STUB_COUNTER"]
+k = int(open(ctr).read()) if os.path.exists(ctr) else 0
+open(ctr, "w").write(str(k + 1))
+plan = os.environ["STUB_PLAN"].split(",")
+what = plan[k] if k < len(plan) else "ok"
+env_seen = {key: os.environ.get(key) for key in ("HICCL_STREAM_ORDERED", "GPU_MAX_HW_QUEUES", "HICCL_STEP_PROGRAM")}
+if what in ("ok", "katfail"):
+    with open(os.environ["HICCL_DRIVER_JSON"], "w") as f:
+        json.dump({"kat": "PASSED" if what == "ok" else "FAILED", "collective_ms_median": 2.0 + k,
+                   "mode_used": "stub", "env_seen": env_seen, "argv": sys.argv[1:]}, f)
+    sys.exit(0 if what == "ok" else 1)
+sys.exit({"killed": 124, "sigkill": 137, "crash": 139}[what])
+'''
+
+
+def _stub_leg(tmp_path, monkeypatch, plan):
+    import argparse
+    sys.path.insert(0, ROOT)
+    import bench
+    stub = tmp_path / "mpirun"
+    stub.write_text(f"#!{sys.executable}\n" + STUB_MPIRUN)
+    stub.chmod(0o755)
+    exe = tmp_path / "collectives_stub"
+    exe.write_text("")
+    monkeypatch.setattr(bench, "C5_MPIRUN", str(stub))
+    monkeypatch.setattr(bench, "C5_EXE", str(exe))
+    monkeypatch.setattr(bench, "visible_gpus", lambda env: 0)
+    monkeypatch.setenv("STUB_PLAN", ",".join(plan))
+    monkeypatch.setenv("STUB_COUNTER", str(tmp_path / "ctr"))
+    return bench, argparse.Namespace(c5_log2count=10, c5_iters=1)
+
+
+def test_c5_leg_failed_kat_lets_next_mode_run(tmp_path, monkeypatch):
+    """A mode whose MPI job exits 1 (its known-answer check failed, or its
+    own signal time-out) leaves the GPUs usable: the leg records it and runs
+    the next mode (bench.run_c5; stub launcher in place of mpirun)."""
+    bench, args = _stub_leg(tmp_path, monkeypatch, ["ok", "katfail", "ok", "ok", "ok", "ok", "ok"])
+    res = bench.run_c5(4, args, allow_shared=True)
+    assert res["host"]["kat"] == "PASSED" and res["host"]["rc"] == 0
+    assert res["stream_graph"]["kat"] == "FAILED" and res["stream_graph"]["rc"] == 1
+    assert res["stream_graph_fused_noprog"]["kat"] == "PASSED"
+    assert "stopped_after" not in res
+    assert all(res[m]["rc"] == 0 for m in ("stream_graph_fused_fenced", "flat_stream_graph_fused", "xccl",
+                                          "stream_graph_fused"))
+    assert res["protocol_ab"]["baseline_kat"] == "PASSED"
+    # a rehearsal on a shared GPU: 2 hardware queues per rank; the stream
+    # modes ask for stream-ordered mode as "1" (the library falls back)
+    assert res["stream_graph"]["env_seen"] == {"HICCL_STREAM_ORDERED": "1", "GPU_MAX_HW_QUEUES": "2",
+                                               "HICCL_STEP_PROGRAM": "0"}
+
+
+@pytest.mark.parametrize("rc_kind", ["killed", "sigkill", "crash"])
+def test_c5_leg_killed_mode_stops_the_leg(tmp_path, monkeypatch, rc_kind):
+    """A mode killed at its limit (124 / 137) or crashed (139) stops the leg:
+    `stopped_after` names it, nothing more starts on the GPUs, and the leg
+    still returns its record (the replica headline is computed after it)."""
+    bench, args = _stub_leg(tmp_path, monkeypatch, ["ok", "ok", rc_kind])
+    res = bench.run_c5(8, args, allow_shared=True)
+    assert res["stopped_after"] == "stream_graph_fused_noprog"
+    assert res["stream_graph_fused_noprog"]["rc"] == {"killed": 124, "sigkill": 137, "crash": 139}[rc_kind]
+    assert "error" in res["stream_graph_fused_noprog"]  # no JSON from a killed job
+    for later in ("stream_graph_fused_fenced", "flat_stream_graph_fused", "xccl", "stream_graph_fused"):
+        assert later not in res
+    assert int((tmp_path / "ctr").read_text()) == 3  # no launch after the killed one
+    assert res["protocol_ab"]["baseline_ms"] is None
+
+
+def test_c5_leg_force_stream_rehearsal(tmp_path, monkeypatch):
+    """--c5-force-stream: the stream-ordered modes ask for
+    HICCL_STREAM_ORDERED=force (run stream-ordered even with ranks sharing a
+    GPU); host-driven and xccl modes keep 0; refused outside a rehearsal."""
+    bench, args = _stub_leg(tmp_path, monkeypatch, ["ok"] * 7)
+    res = bench.run_c5(8, args, allow_shared=True, force_stream=True,
+                       only=("host", "stream_graph_fused_noprog", "xccl"))
+    assert res["forced_stream_ordered"] is True
+    assert res["host"]["env_seen"]["HICCL_STREAM_ORDERED"] == "0"
+    assert res["stream_graph_fused_noprog"]["env_seen"]["HICCL_STREAM_ORDERED"] == "force"
+    assert res["xccl"]["env_seen"]["HICCL_STREAM_ORDERED"] == "0"
+    assert "skipped" in bench.run_c5(8, args, allow_shared=False, force_stream=True)
+
+
+def _c5_leg_raises(port, q):
+    os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import argparse
+
+    import bench
+
+    def boom(*a, **k):
+        raise RuntimeError("stub failure")
+    bench.run_c5 = boom
+    res = bench.c5_leg(argparse.Namespace(c5_log2count=10, c5_iters=1))
+    d = bench.Dist(1)
+    q.put(res)
+    d.close()
+
+
+def test_c5_leg_error_never_costs_the_headline():
+    """An exception inside the config-5 leg becomes a `skipped` record; the
+    control plane survives for the replica measurement that follows."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_c5_leg_raises, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert res == {"skipped": "error: stub failure"}

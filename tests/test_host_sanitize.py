@@ -82,4 +82,4 @@ def test_driver_json_and_step_timing_clean(tmp_path):
     assert "Sanitizer" not in out and "runtime error" not in out, out[-3000:]
     assert p.returncode == 0, out[-3000:]
     r = json.loads(path.read_text())
-    assert r["kat"] == "PASSED" and r["host_split_us_per_step"]["runs"] == 2
+    assert r["kat"] == "PASSED" and r["host_split_us_per_step"]["runs"] == 1

@@ -205,9 +205,10 @@ extern "C" {
 // mode: 0 mix (N reads + 1 write), 1 read-only, 2 write-only, 3 LDS-DMA mix
 int probe_run(int mode, int block, int unroll, int aux_load, int aux_store, int order, int grid,
               const void *const *in, int n, void *out, uint64_t bytes, void *stream) {
-  // the kernels read p.in[0..n): at most 64 streams (8 for the LDS and
-  // grouped mixes), as many as config 3's largest bucket
-  if (n < 1 || n > 64 || (mode == 3 && n > 8)) return -1;
+  // the kernels read p.in[0..n): at most 64 streams (at most 8 for the LDS
+  // mix; exactly 8 for the grouped mix, whose loads are unrolled over 8
+  // inputs), as many as config 3's largest bucket
+  if (n < 1 || n > 64 || (mode == 3 && n > 8) || (mode == 4 && n != 8)) return -1;
   Ptrs p;
   for (int k = 0; k < 64; k++) p.in[k] = (const char *)(k < n ? in[k] : in[0]);
   p.out = (char *)out;
@@ -215,7 +216,7 @@ int probe_run(int mode, int block, int unroll, int aux_load, int aux_store, int 
   p.n = n;
   hipStream_t s = (hipStream_t)stream;
   if (mode == 4) {  // grouped mix: unroll = U, order = G
-    if (n > 8 || block != 256) return -1;
+    if (block != 256) return -1;
     const int key = unroll * 10 + order;
     switch (key) {
       case 41: return launch(k_mix_grp<256, 4, 1>, grid, 256, p, s);
