@@ -539,6 +539,65 @@ def cgroup_cpu_stat():
     return st
 
 
+def host_cpu_busy():
+    """(busy, total) jiffies of the whole host from /proc/stat's first line
+    (every CPU, every tenant): the share of the host's CPUs busy between two
+    reads, this process included."""
+    f = (_read("/proc/stat") or "cpu 0 0 0 1").splitlines()[0].split()[1:]
+    v = [int(x) for x in f[:8]]
+    idle = v[3] + (v[4] if len(v) > 4 else 0)
+    return sum(v) - idle, sum(v)
+
+
+def vmstat(keys=("numa_pages_migrated", "pgmigrate_success", "numa_hint_faults", "thp_fault_alloc",
+                 "thp_collapse_alloc")):
+    st = {}
+    for line in (_read("/proc/vmstat") or "").splitlines():
+        k, _, v = line.partition(" ")
+        if k in keys:
+            st[k] = int(v)
+    return st
+
+
+def cpu_node(c):
+    base = f"/sys/devices/system/cpu/cpu{c}"
+    return next((int(e[4:]) for e in (os.listdir(base) if c >= 0 and os.path.isdir(base) else [])
+                 if e.startswith("node") and e[4:].isdigit()), None)
+
+
+def numa_locality(bufs, thread_cpus, per_block=32):
+    """How many of the pages each OpenMP thread sums sit on its own NUMA
+    node: reduce_kernel's `omp parallel for` (libgomp's static schedule)
+    gives thread t one contiguous block of every buffer; 32 pages per block
+    and buffer are located with move_pages(2) (query only).  Returns the
+    local fraction and the page count per node, or None if the query fails."""
+    libc = ctypes.CDLL(None, use_errno=True)
+    T = len(thread_cpus)
+    addrs, want = [], []
+    for b in bufs:
+        count, base = b.size, b.ctypes.data
+        q, r = divmod(count, T)
+        for t, c in enumerate(thread_cpus):
+            lo = q * t + min(t, r)
+            hi = lo + q + (1 if t < r else 0)
+            for j in range(per_block):
+                i = lo + (hi - lo) * j // per_block
+                addrs.append((base + 4 * i) & ~4095)
+                want.append(cpu_node(c))
+    n = len(addrs)
+    pages = (ctypes.c_void_p * n)(*addrs)
+    status = (ctypes.c_int * n)()
+    rc = libc.syscall(ctypes.c_long(279), ctypes.c_int(0), ctypes.c_ulong(n), pages, None, status, ctypes.c_int(0))
+    if rc != 0:
+        return None
+    got = list(status)
+    hist = {}
+    for g in got:
+        hist[str(g)] = hist.get(str(g), 0) + 1
+    ok = sum(1 for g, w in zip(got, want) if g >= 0 and g == w)
+    return {"local_frac": round(ok / n, 4), "pages_sampled": n, "pages_per_node": hist}
+
+
 def places_desc():
     pl = os.environ.get("OMP_PLACES", "")
     return f"{len(pl.split(','))} explicit places" if pl.startswith("{") else f"OMP_PLACES={pl}"
@@ -575,6 +634,10 @@ def cpu_leg(args):
     out = np.empty(count, np.float32)
     fill(out.ctypes.data, count, SEED, 99, 0)  # first touch of the output
     tab = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+    tc = (ctypes.c_int * 512)()
+    team = ora.oracle_thread_cpus(tc, 512)
+    thread_cpus = list(tc)[:team]
+    local0 = numa_locality(bufs + [out], thread_cpus)
 
     def one():
         t = time.perf_counter()
@@ -585,14 +648,19 @@ def cpu_leg(args):
         return time.perf_counter() - t
 
     one()  # warm
-    times, thr = [], []
+    times, thr, busy = [], [], []
     st0 = st = cgroup_cpu_stat()
+    vm0, hb0 = vmstat(), host_cpu_busy()
+    hb = hb0
     t_start = time.perf_counter()
     while time.perf_counter() - t_start < args.cpu_budget and len(times) < 50:
         times.append(one())
-        st1 = cgroup_cpu_stat()
+        st1, hb1 = cgroup_cpu_stat(), host_cpu_busy()
         thr.append(round((st1.get("throttled_usec", 0) - st.get("throttled_usec", 0)) * 1e-3, 2))
-        st = st1
+        busy.append(round((hb1[0] - hb[0]) / max(1, hb1[1] - hb[1]), 3))
+        st, hb = st1, hb1
+    vm1 = vmstat()
+    local1 = numa_locality(bufs + [out], thread_cpus)
     med = float(np.median(times))
     rate = lambda t: round((n + 1) * count * 4 / t / 1e9, 2)  # noqa: E731
     # the spread over the passes, as the reference prints min / median / max
@@ -605,6 +673,14 @@ def cpu_leg(args):
            "min": rate(max(times)), "max": rate(min(times)), "max_over_min": round(slow, 3), "passes": len(times),
            "pass_ms": [round(t * 1e3, 2) for t in times], "throttle": throttle,
            "throttled_ms": thr if st0 else None,
+           # the whole host's CPU busy share per pass (/proc/stat: every
+           # tenant; this leg's own threads are threads / host CPUs of it)
+           "host_busy_frac": busy, "host_cpus": os.cpu_count(),
+           "thread_cpus": thread_cpus, "numa_locality_before": local0, "numa_locality_after": local1,
+           "vmstat_delta": {k: vm1.get(k, 0) - vm0.get(k, 0) for k in vm1},
+           "numa_balancing": _read("/proc/sys/kernel/numa_balancing"),
+           "thp": _read("/sys/kernel/mm/transparent_hugepage/enabled"),
+           "cpuset_mems": _read("/sys/fs/cgroup/cpuset.mems.effective"),
            "sample": f"{n} x 2^{args.log2count} fp32 -> 1 output (the full config-2 bucket), median of "
                      f"{len(times)} passes ({med * 1e3:.1f} ms each), OpenMP {threads} threads "
                      f"(OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND', '')}, "

@@ -34,6 +34,8 @@
  * the GPU fill kernel, this oracle and the fixtures agree without
  * transferring data.
  */
+#define _GNU_SOURCE /* sched_getcpu: oracle_thread_cpus */
+#include <sched.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
@@ -196,4 +198,26 @@ int oracle_num_threads(void) {
 #else
   return 1;
 #endif
+}
+
+/* The CPU each thread of an OpenMP team runs on (out[t] for thread t < n,
+ * -1 where unknown): where bench.py's CPU baseline leg put the threads
+ * whose static blocks it then checks for NUMA locality.  Returns the team
+ * size. */
+int oracle_thread_cpus(int *out, int n) {
+  int team = 1;
+  for (int t = 0; t < n; t++) out[t] = -1;
+#ifdef _OPENMP
+  extern int omp_get_thread_num(void);
+  extern int omp_get_num_threads(void);
+  #pragma omp parallel
+  {
+    const int t = omp_get_thread_num();
+    if (t < n) out[t] = sched_getcpu();
+    if (t == 0) team = omp_get_num_threads();
+  }
+#else
+  out[0] = sched_getcpu();
+#endif
+  return team;
 }
