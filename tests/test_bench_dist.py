@@ -324,3 +324,33 @@ def test_c5_leg_error_never_costs_the_headline():
     p.join(timeout=60)
     assert p.exitcode == 0
     assert res == {"skipped": "error: stub failure"}
+
+
+def test_cpu_placement_one_thread_per_l3_first():
+    """The CPU baseline's explicit OMP_PLACES: `l3spread` takes one core per
+    L3 domain (CCD) across every NUMA node before a second core of any;
+    `node` does the same inside the node holding the most cores."""
+    sys.path.insert(0, ROOT)
+    import bench
+    # 2 nodes x 2 CCDs x 4 cores, CPU c on CCD c // 4, node c // 8
+    cores = [{"cpu": c, "pkg": str(c // 8), "node": c // 8, "l3": str(c // 4)} for c in range(16)]
+    assert bench.cpu_placement(cores, 4, "l3spread") == [0, 4, 8, 12]
+    assert bench.cpu_placement(cores, 6, "l3spread") == [0, 4, 8, 12, 1, 5]
+    assert bench.cpu_placement(cores, 4, "node") == [0, 4, 1, 5]
+    assert bench.cpu_placement(cores, 99, "l3spread") == sorted(range(16), key=lambda c: (c % 4, c // 4))
+
+
+def test_cpu_spread_cause_names_what_the_leg_saw():
+    """cpu_baseline's spread_cause: quota throttling when it covers most of
+    the slow passes' excess; otherwise, with local pages, no migration and
+    an idle host, bandwidth taken outside the container, in runs of passes."""
+    sys.path.insert(0, ROOT)
+    import bench
+    loc = {"local_frac": 1.0}
+    t = [0.022] * 10 + [0.060] * 5 + [0.022] * 5
+    r = bench.spread_cause(t, [0.0] * 20, [0.1] * 20, loc, loc, {}, 16)
+    assert r["slow_passes"] == 5 and r["slow_runs"] == 1 and r["cause"].startswith("host memory bandwidth")
+    r = bench.spread_cause(t, [0.0] * 10 + [38.0] * 5 + [0.0] * 5, [0.1] * 20, loc, loc, {}, 16)
+    assert r["cause"] == "cgroup CPU quota throttling" and r["throttle_covers_frac"] == 1.0
+    r = bench.spread_cause(t, None, [0.1] * 20, {"local_frac": 0.5}, loc, {}, 16)
+    assert r["cause"].startswith("unnamed") and r["pages_local"] is False
