@@ -206,9 +206,9 @@ extern "C" {
 int probe_run(int mode, int block, int unroll, int aux_load, int aux_store, int order, int grid,
               const void *const *in, int n, void *out, uint64_t bytes, void *stream) {
   // the kernels read p.in[0..n): at most 64 streams (at most 8 for the LDS
-  // mix; exactly 8 for the grouped mix, whose loads are unrolled over 8
-  // inputs), as many as config 3's largest bucket
-  if (n < 1 || n > 64 || (mode == 3 && n > 8) || (mode == 4 && n != 8)) return -1;
+  // and grouped mixes, whose loads are unrolled over 8 inputs; fewer read
+  // zeros through empty descriptors), as many as config 3's largest bucket
+  if (n < 1 || n > 64 || ((mode == 3 || mode == 4) && n > 8)) return -1;
   Ptrs p;
   for (int k = 0; k < 64; k++) p.in[k] = (const char *)(k < n ? in[k] : in[0]);
   p.out = (char *)out;
