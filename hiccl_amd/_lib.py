@@ -89,6 +89,7 @@ _SIGS = {
     "hiccl_reduce_plan_engine": (ctypes.c_int, [_vp]),
     "hiccl_reduce_plan_set_peer": (ctypes.c_int, [_vp, ctypes.c_int]),
     "hiccl_reduce_plan_peer": (ctypes.c_int, [_vp]),
+    "hiccl_reduce_plan_store_policy": (ctypes.c_int, [_vp]),
     "hiccl_reduce_plan_add": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_size_t]),
     "hiccl_reduce_plan_launch": (ctypes.c_int, [_vp, _vp]),
     "hiccl_reduce_plan_enqueue": (ctypes.c_int, [_vp, _vp]),

@@ -149,6 +149,11 @@ class Compute:
     def peer(self):
         return L.lib().hiccl_reduce_plan_peer(self._plan)
 
+    def store_policy(self):
+        """The store form of the plan's launches (hiccl_reduce_plan_store_policy):
+        2 nt, 4 system-scope write-through."""
+        return L.lib().hiccl_reduce_plan_store_policy(self._plan)
+
     def engine(self):
         """Engine the last upload resolved to (HICCL_ENGINE_TILE / _PHASE)."""
         return L.lib().hiccl_reduce_plan_engine(self._plan)

@@ -1509,8 +1509,9 @@ plan_fn pick_plan(int dtype, int acc, int engine, int unroll, int pol = kDefPol)
 // Is `c` (engine resolved, shape filled in by finish_cfg) a shape the plan
 // kernels have?  Empty string if so, else why not.
 std::string plan_shape_error(const Cfg &c, int dtype) {
-  if (c.nt != kDefPol % 10 || c.store != kDefPol / 10)
-    return "plan kernels use nt loads and nt stores only (nontemporal 2, store_policy 2)";
+  if (c.nt != kDefPol % 10 || (c.store != kDefPol / 10 && c.store != kPolStoreSys))
+    return "plan kernels load nt (nontemporal 2) and store nt (store_policy 2), system-scope write-through "
+           "(store_policy 4) or either by the launch's size (store_policy 0)";
   if (c.drain) return "plan kernels do not support drain";
   if (c.engine == HICCL_ENGINE_PHASE) {
     if (c.block != kPhBlock || c.unroll != phase_p_dtype(dtype, c.acc))
@@ -1662,6 +1663,7 @@ struct hiccl_reduce_plan {
   double mean_n = 0;               // packet-weighted inputs per compute
   int bpc = 1;                     // workgroups per CU, resolved at upload
   int peer = 0;                    // hiccl_reduce_plan_set_peer flags
+  int eff_peer = 0;                // peer | the store form plan_store_peer picks, resolved at upload
   size_t esz = 0;
   struct Comp {
     void *out;
@@ -1694,14 +1696,45 @@ void plan_quiesce(hiccl_reduce_plan *p) {
 
 namespace {
 
+// Store form of a plan's launches.  nt stores are not write-through: a
+// launch's output lines may sit dirty in the XCD L2s until the end-of-kernel
+// release writes them back, on the critical path of the next kernel on the
+// stream (MI355X_MICROARCH.md "boundary": + B / 6 TB/s for B dirty bytes).
+// So a plan that writes at most kPlanWtMaxBytes per launch stores with
+// system-scope write-through (sc0 sc1, the peer-store form) instead, when its
+// config leaves the store form to size (store_policy 0).  Measured on the C5
+// step (4 x n = 2 + 1 x n = 4 computes of 2^18 f32, 5 MiB written, plus its
+// five 1 MiB byte copies; tools/step_store_probe.py,
+// profiles/r05d_step_store.jsonl): the reduction 4.52 -> 3.53 us per eager
+// launch (0.49 -> 0.63 of 8 TB/s), 3.01 -> 2.91 us under graph replay, the
+// copies 3.53 -> 3.28 us; 10-20 MiB written 20-38 % faster; at 80 MiB the
+// reduction still 3 % faster but the copies 4.5 % slower -- hence the cap.
+constexpr uint64_t kPlanWtMaxBytes = 32ull << 20;
+
+int plan_store_peer(const hiccl_reduce_plan *p) {
+  const int req = p->req.store_policy;  // 0: by size; 2: nt; 4: write-through (plan_set_config checked it)
+  if (req == kPolStoreSys + 1) return HICCL_PEER_STORES;
+  if (req != 0) return 0;
+  // by size only where a write-through kernel of the plan's shape exists: an
+  // explicit TILE unroll other than 2 / 4 keeps nt stores
+  const int u = p->req.unroll;
+  if (u && u != 2 && u != kDefUnroll && p->req.engine != HICCL_ENGINE_PHASE) return 0;
+  uint64_t out = 0;
+  for (auto &c : p->comps) out += (uint64_t)c.count * p->esz;
+  return out <= kPlanWtMaxBytes ? HICCL_PEER_STORES : 0;
+}
+
+int plan_eff_peer(const hiccl_reduce_plan *p) { return p->peer | plan_store_peer(p); }
+
 // The plan's configuration with its engine and shape resolved for `npkt`
 // packets of packet-weighted mean `mean_n` inputs.
 Cfg plan_cfg(const hiccl_reduce_plan *p, uint64_t npkt, double mean_n) {
   Cfg c = resolve(&p->req);
   const bool auto_unroll = !c.unroll;
   finish_cfg(c, npkt, mean_n, p->dtype, p->device);  // (kPlanBlock == kDefBlock)
-  // peer policies exist at TILE U = 4 / 2 only: wide tiles become U = 4
-  if (p->peer && c.engine == HICCL_ENGINE_TILE && auto_unroll && c.unroll != 2) c.unroll = kDefUnroll;
+  // peer and write-through policies exist at TILE U = 4 / 2 only: wide tiles
+  // become U = 4
+  if (p->eff_peer && c.engine == HICCL_ENGINE_TILE && auto_unroll && c.unroll != 2) c.unroll = kDefUnroll;
   return c;
 }
 
@@ -1743,6 +1776,7 @@ int plan_upload(hiccl_reduce_plan *p, hipStream_t s) {
   }
   const double mean_n = total_pkt ? weighted_n / total_pkt : 0;
   p->mean_n = mean_n;
+  p->eff_peer = plan_eff_peer(p);
   const Cfg c = plan_cfg(p, total_pkt, mean_n);
   p->engine = c.engine;
   p->unroll = c.unroll;
@@ -1810,7 +1844,7 @@ int plan_kernel(hiccl_reduce_plan *p, hipStream_t s) {
   c.unroll = p->unroll;
   c.block = p->engine == HICCL_ENGINE_PHASE ? kPhBlock : kPlanBlock;
   c.bpc = p->bpc;
-  return launch_plan(p->args, p->dtype, c, p->mean_n, p->device, s, plan_pol(p->peer));
+  return launch_plan(p->args, p->dtype, c, p->mean_n, p->device, s, plan_pol(p->eff_peer));
 }
 
 int reduce_via_table(int dtype, const Cfg &c, void *out, const void *const *in, int n, size_t count,
@@ -1843,7 +1877,9 @@ int reduce_via_table(int dtype, const Cfg &c, void *out, const void *const *in, 
   a.stride = (uint32_t)n;
   a.t_begin = 0;
   a.t_end = tiles_for(sp.npkt, unit_pkts(c.engine, dtype, c.acc, c.unroll));
-  if (int e = launch_plan(a, dtype, c, n, current_device(), s)) return e;
+  // (one-shot: nt stores unless the caller asked for write-through, store_policy 4)
+  const int pol = c.store == kPolStoreSys ? plan_pol(HICCL_PEER_STORES) : kDefPol;
+  if (int e = launch_plan(a, dtype, c, n, current_device(), s, pol)) return e;
   return check_hip(hipFreeAsync(dmem, s), "hiccl_reduce: hipFreeAsync");
 }
 
@@ -1898,6 +1934,11 @@ int hiccl_reduce_plan_set_peer(hiccl_reduce_plan_t *p, int flags) {
 }
 
 int hiccl_reduce_plan_peer(const hiccl_reduce_plan_t *p) { return p ? p->peer : -1; }
+
+int hiccl_reduce_plan_store_policy(const hiccl_reduce_plan_t *p) {
+  if (!p) return -1;
+  return (plan_eff_peer(p) & HICCL_PEER_STORES) ? kPolStoreSys + 1 : kDefPol / 10 + 1;
+}
 
 int hiccl_reduce_plan_set_config(hiccl_reduce_plan_t *p, const hiccl_reduce_config_t *cfg) {
   if (!p) return fail(hipErrorInvalidValue, "plan_set_config: plan is NULL");
@@ -2463,7 +2504,8 @@ int hiccl_program_add_plan(hiccl_program_t *p, const hiccl_reduce_plan_t *plan) 
     return fail(hipErrorInvalidValue, "program_add_plan: the plan's dtype is neither the program's nor HICCL_BYTES");
   if (plan->req.acc == HICCL_ACC_WIDE)
     return fail(hipErrorInvalidValue, "program_add_plan: programs accumulate natively (HICCL_ACC_NATIVE) only");
-  for (auto &c : plan->comps) p->units.push_back(hiccl_program::Unit{c.out, c.in, c.count, bytes, plan->peer});
+  const int peer = plan_eff_peer(plan);  // the plan's own store form (plan_store_peer) carries over
+  for (auto &c : plan->comps) p->units.push_back(hiccl_program::Unit{c.out, c.in, c.count, bytes, peer});
   p->dirty = true;
   return 0;
 }

@@ -135,7 +135,10 @@ typedef struct {
   int nontemporal;   /* loads: 1 plain cache policy, 2 nt */
   int acc;           /* hiccl_acc_t */
   int grid;          /* total workgroups; overrides blocks_per_cu when > 0 */
-  int store_policy;  /* stores: 1 plain, 2 nt, 3 sc1 (write-through, line dropped from L2) */
+  int store_policy;  /* stores: 1 plain, 2 nt, 3 sc1 (write-through, line dropped from L2),
+                        4 system-scope write-through (sc0 sc1; plans only).  0: nt for a
+                        one-shot call; for a plan, 4 when a launch writes at most 32 MiB
+                        (no dirty L2 lines left for the kernel boundary), else 2 */
   int engine;        /* hiccl_engine_t */
   int schedule;      /* hiccl_schedule_t */
   int grab;          /* dynamic schedule: units per ticket (0 = default: PHASE 1,
@@ -192,9 +195,14 @@ int hiccl_reduce_plan_set_engine(hiccl_reduce_plan_t *plan, int engine);
 /* Kernel configuration of the plan's launches (NULL = all defaults; replaces
  * earlier set_engine / set_acc choices).  Honoured: engine, schedule, grab,
  * blocks_per_cu, grid, acc, and the TILE shape block 256 x unroll 4 (f32 and
- * bf16 also unroll 1, 2, 8 or 16); PHASE runs its default shape; loads and stores
- * are nt.  Anything else is refused with hipErrorInvalidValue -- no field is
- * silently ignored. */
+ * bf16 also unroll 1, 2, 8 or 16); PHASE runs its default shape; loads are
+ * nt; stores are nt (store_policy 2), system-scope write-through (4), or
+ * (0, the default) write-through when a launch writes at most 32 MiB and nt
+ * above -- the pipeline-step sizes, where nt lines left dirty in the L2s
+ * cost the kernel boundary their write-back -- except
+ * for an explicit TILE unroll 1, 8 or 16, which stays nt.  Write-through
+ * runs the shapes the peer kernels have (below).  Anything else is refused
+ * with hipErrorInvalidValue -- no field is silently ignored. */
 int hiccl_reduce_plan_set_config(hiccl_reduce_plan_t *plan, const hiccl_reduce_config_t *cfg);
 /* Peer memory.  The transport's data movement (the CommBench IPC put / get
  * the reference registers at command.h:122,132 and starts at comm.h:190,197)
@@ -219,6 +227,10 @@ typedef enum {
 int hiccl_reduce_plan_set_peer(hiccl_reduce_plan_t *plan, int flags);
 /* The plan's peer flags (-1 for NULL). */
 int hiccl_reduce_plan_peer(const hiccl_reduce_plan_t *plan);
+/* The store form the plan's launches take with its current computes and
+ * config (hiccl_reduce_config_t.store_policy: 2 nt, 4 system-scope
+ * write-through; -1 for NULL). */
+int hiccl_reduce_plan_store_policy(const hiccl_reduce_plan_t *plan);
 /* The engine the last upload resolved to (TILE before the first launch). */
 int hiccl_reduce_plan_engine(const hiccl_reduce_plan_t *plan);
 int hiccl_reduce_plan_add(hiccl_reduce_plan_t *plan, void *out, const void *const *in, int n,

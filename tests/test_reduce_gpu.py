@@ -895,9 +895,74 @@ def test_plan_peer_policy_replaces_wide_tiles(oracle):
     comp.close()
 
 
+@pytest.mark.parametrize("cfg,want", [(None, 4), (dict(store_policy=2), 2), (dict(store_policy=4), 4),
+                                      (dict(engine=2), 4), (dict(engine=1, unroll=2), 4),
+                                      (dict(engine=1, unroll=1), 2)],
+                         ids=["auto", "nt", "wt", "phase", "u2", "u1-nt"])
+def test_plan_store_form_small_step(oracle, cfg, want):
+    """A pipeline step's plan (the C5 step: 4 computes of n = 2 and one of
+    n = 4, 2^18 f32, 5 MiB written) stores write-through by default -- nt
+    lines left dirty in the L2s would cost the kernel boundary their
+    write-back -- unless its config asks for nt or a shape only the nt
+    kernels have; every form gives the oracle's bits, relaunched."""
+    c = 1 << 18
+    x = oracle.fill(12, c, seed=1212)
+    ins = [to_dev(r) for r in x]
+    outs = [torch.full((c,), float("nan"), device=DEV) for _ in range(5)]
+    comp = hiccl_amd.Compute(torch.float32, device=0, config=cfg)
+    for j in range(4):
+        comp.add([ins[2 * j], ins[2 * j + 1]], outs[j], c, compid=0)
+    comp.add(ins[8:12], outs[4], c, compid=0)
+    assert comp.store_policy() == want
+    exps = [oracle.reduce([x[2 * j], x[2 * j + 1]]) for j in range(4)] + [oracle.reduce(list(x[8:12]))]
+    for _ in range(2):
+        comp.start()
+        comp.wait()
+        for o, e in zip(outs, exps):
+            assert bits_equal(o.cpu().numpy(), e)
+    comp.close()
+
+
+@pytest.mark.parametrize("cfg,want", [(None, 2), (dict(store_policy=4), 4)], ids=["auto-nt", "wt"])
+def test_plan_store_form_large(oracle, cfg, want):
+    """Above 32 MiB written per launch the default is nt (at 80 MiB the
+    step's byte copies ran 4.5 % slower write-through); write-through on
+    request; sampled-exact at 8 inputs x 64 MiB in 1 MiB computes."""
+    n, count, seed = 8, 1 << 24, 808
+    ins = [torch.empty(count, device=DEV) for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, seed, k)
+    out = torch.empty(count, device=DEV)
+    comp = hiccl_amd.Compute(torch.float32, device=0, config=cfg)
+    step = 1 << 18
+    for off in range(0, count, step):
+        comp.add([(t, off) for t in ins], (out, off), step, compid=0)
+    assert comp.store_policy() == want
+    comp.start()
+    comp.wait()
+    ok, msg = _sampled(out, n, count, seed)
+    assert ok, msg
+    comp.close()
+
+
+def test_byte_copy_plan_small_is_write_through():
+    """The transport's per-step copies (HICCL_BYTES plans, 1 MiB each) take
+    the write-through form too, exact."""
+    comp = hiccl_amd.Compute(torch.uint8, device=0)
+    src = [torch.randint(0, 256, ((1 << 20) + 3,), dtype=torch.uint8, device=DEV) for _ in range(5)]
+    dst = [torch.zeros((1 << 20) + 3, dtype=torch.uint8, device=DEV) for _ in range(5)]
+    for a, b in zip(src, dst):
+        comp.add([a], b, (1 << 20) + 3, compid=0)
+    assert comp.store_policy() == 4
+    comp.start()
+    comp.wait()
+    assert all(torch.equal(a, b) for a, b in zip(src, dst))
+    comp.close()
+
+
 def test_plan_config_refuses_unsupported_fields():
     for bad in (dict(engine=1, unroll=32), dict(engine=1, unroll=3), dict(engine=2, unroll=4), dict(engine=1, block=512),
-                dict(nontemporal=1), dict(store_policy=3), dict(drain=1), dict(schedule=7)):
+                dict(nontemporal=1), dict(store_policy=3), dict(store_policy=1), dict(drain=1), dict(schedule=7)):
         with pytest.raises(hiccl_amd.HicclError):
             hiccl_amd.Compute(torch.float32, device=0, config=bad)
     with pytest.raises(hiccl_amd.HicclError):  # unroll 2 exists for f32/bf16 only

@@ -8,9 +8,8 @@ table (MI355X_MICROARCH.md "boundary") adds B / 6 TB/s to a kernel boundary
 when the predecessor leaves B bytes dirty.  nt stores are not write-through:
 the step's 5 MiB of outputs may sit dirty in the XCD L2s until the
 end-of-kernel release writes them back.  This probe times the same plan
-with the plan kernels' default nt stores and with system-scope write-through
-stores (hiccl_reduce_plan_set_peer(HICCL_PEER_STORES): the peer-store
-policy, sc0 sc1), queued (events around 200 back-to-back launches) and as
+with nt stores (store_policy 2) and with system-scope write-through
+stores (store_policy 4: the peer-store form, sc0 sc1), queued (events around 200 back-to-back launches) and as
 one hipGraph of 200 launches, at scales 1/4 .. 16, interleaved rounds; and
 the step's copies (5 x 1 MiB byte plans) the same way.  Both policies must
 give the same bits.  One JSON line per scale, then a summary.
@@ -29,25 +28,24 @@ sys.path.insert(0, ROOT)
 
 import bench as B  # noqa: E402
 import hiccl_amd  # noqa: E402
-from hiccl_amd import _lib as L  # noqa: E402
 
 
 def step_plan(dev, bufs, outs, c, peer):
-    comp = hiccl_amd.Compute(torch.float32, device=dev)
+    # explicit store forms: 2 nt, 4 write-through (round 5's default picks
+    # by size; this probe is what set it)
+    comp = hiccl_amd.Compute(torch.float32, device=dev, config=dict(store_policy=4 if peer else 2))
     for j in range(4):
         comp.add([bufs[2 * j], bufs[2 * j + 1]], outs[j], c, compid=0)
     comp.add(bufs[8:12], outs[4], c, compid=0)
-    if peer:
-        comp.set_peer(L.HICCL_PEER_STORES)
+    assert comp.store_policy() == (4 if peer else 2)
     return comp
 
 
 def copy_plan(dev, src, dst, nbytes, peer):
-    cp = hiccl_amd.Compute(torch.uint8, device=dev)
+    cp = hiccl_amd.Compute(torch.uint8, device=dev, config=dict(store_policy=4 if peer else 2))
     for a, b in zip(src, dst):
         cp.add([a.view(torch.uint8)], b.view(torch.uint8), nbytes, compid=0)
-    if peer:
-        cp.set_peer(L.HICCL_PEER_STORES)
+    assert cp.store_policy() == (4 if peer else 2)
     return cp
 
 
@@ -75,7 +73,7 @@ def graph_us(fn, n=200):
 def main():
     dev = torch.cuda.current_device()
     stream = torch.cuda.current_stream()
-    scales = (0.25, 0.5, 1, 2, 4, 16)
+    scales = (0.25, 0.5, 1, 2, 4, 8, 16)
     cases = {}
     for f in scales:
         c = int((1 << 18) * f)
