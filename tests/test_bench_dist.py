@@ -354,3 +354,55 @@ def test_cpu_spread_cause_names_what_the_leg_saw():
     assert r["cause"] == "cgroup CPU quota throttling" and r["throttle_covers_frac"] == 1.0
     r = bench.spread_cause(t, None, [0.1] * 20, {"local_frac": 0.5}, loc, {}, 16)
     assert r["cause"].startswith("unnamed") and r["pages_local"] is False
+
+
+def test_driver_line_stays_compact():
+    """bench.py's stdout line carries every contract field and the summaries,
+    and stays a few KB even with a full CPU-baseline record and seven
+    config-5 modes (the driver keeps a tail of stdout; the full record goes
+    to stderr)."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    mode = {"kat": "PASSED", "rc": 0, "collective_ms_median": 31.5, "algorithmic_GBps_median": 34.1,
+            "kernel_us_per_step_rank0": 4.1, "mode_used": "stream-ordered+graph+fused+tokens-fenced",
+            "host_split_us_per_step": {k: 1.0 for k in "abcdefg"}, "bus_ids": ["0000:05:00.0"] * 8,
+            "devices_seen": [8] * 8, "rank_devices": list(range(8)), "pipedepth": 128, "wall_s": 9.1}
+    c5 = {"workload": "C5 ...", "env_scrubbed": {}, "devices_counted_unmasked": 8,
+          **{k: dict(mode) for k in ("host", "stream_graph", "stream_graph_fused_noprog", "stream_graph_fused_fenced",
+                                     "flat_stream_graph_fused", "xccl", "stream_graph_fused")}}
+    c5["xccl"] = {"error": "rc 124: " + "x" * 600, "rc": 124, "wall_s": 120.0}
+    c5["stopped_after"] = "xccl"
+    c5["protocol_ab"] = bench.c5_protocol_ab(c5)
+    cpu = {"value": 400.0, "unit": "GB/s", "cores": 16, "kind": "reference", "min": 150.0, "max": 440.0,
+           "max_over_min": 2.9, "passes": 50, "pass_ms": [22.123] * 50, "throttled_ms": [0.0] * 50,
+           "host_busy_frac": [0.123] * 50, "thread_cpus": list(range(16)), "sample": "s" * 300,
+           "placement": {"policy": "l3spread", "cpus": list(range(16)), "numa_nodes": [0, 1], "l3_domains": 16},
+           "throttle": {"nr_periods": 10, "nr_throttled": 0, "throttled_usec": 0},
+           "spread_cause": {"cause": "host memory bandwidth ...", "slow_passes": 20, "slow_runs": 3,
+                            "throttle_covers_frac": 0.0, "pages_local": True, "pages_migrated": 0,
+                            "host_busy_others_median": 0.05}}
+    line = {"metric": bench.METRIC, "value": 6500.0, "unit": "GB/s", "n_gpus": 8, "steps": 20, "warmup": 5,
+            "ms_per_step": 1.48, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic", "config": {"workload": "C2 ..."},
+            "roofline": {"bound": "hbm", "achieved": 6530.0, "peak": 8000.0, "unit": "GB/s", "frac": 0.816,
+                         "traffic": 9.66e9, "serial_rw_model": {"frac": 0.98, "frac_write_probe": 0.95},
+                         "traffic_from_profile": {"file": "profiles/r05b_pmc.json"}, "traffic_source": "x" * 200},
+            "cpu_baseline": cpu, "parity_full": {"ok": True, "mismatches": 0, "words": 1 << 28, "against": "y" * 100},
+            "device_props": {"gcn_arch": "gfx950", "cus": 256, "mem_clock_khz": 2000000},
+            "c2_misaligned": {"shifted_over_aligned": 1.007, "shifted_frac": 0.78,
+                              "parity_sample_ok": {"aligned": True, "shifted": True}}, "c5": c5}
+    out = bench.compact_line(line)
+    text = json.dumps(out)
+    assert len(text) < 3500, len(text)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert out[k] == line[k]
+    r = out["roofline"]
+    assert (r["bound"], r["frac"], r["traffic"], r["serial_rw_frac"]) == ("hbm", 0.816, 9.66e9, 0.95)
+    c = out["cpu_baseline"]
+    assert (c["value"], c["cores"], c["kind"], c["spread_cause"]["slow_runs"]) == (400.0, 16, "reference", 3)
+    assert "pass_ms" not in c and out["c2_misaligned"]["parity_ok"] is True
+    assert out["c5"]["stopped_after"] == "xccl" and out["c5"]["xccl"]["rc"] == 124
+    assert out["c5"]["host"]["kat"] == "PASSED" and "host_split_us_per_step" not in out["c5"]["host"]
+    assert out["c5"]["protocol_ab"]["baseline_ms"] == 31.5

@@ -35,7 +35,7 @@ def nway(args):
                           "GBps": round(b / t / 1e9, 1), "frac_hbm": round(b / t / 1e9 / B.HBM_PEAK_GBPS, 4),
                           "read_GBps": round(n * count * 4 / t / 1e9, 1),
                           "frac_of_copy": round(b / t / 1e9 / copy_gbps, 4),
-                          "B.serial_rw_model": B.serial_rw_model(n * count * 4, count * 4, read_gbps, copy_gbps, t, write_gbps)}),
+                          "serial_rw_model": B.serial_rw_model(n * count * 4, count * 4, read_gbps, copy_gbps, t, write_gbps)}),
               flush=True)
       del ins, out
       torch.cuda.empty_cache()
@@ -81,15 +81,15 @@ def c3_vs_c2(args):
                "ratio_to_c2": round(float(np.median([r / c for r, c in zip(rates, c2_rates)])), 4),
                "read_probe_GBps": round(b["read"], 1) if b["read"] else None,
                "write_probe_GBps": round(b["write"], 1) if b["write"] else None,
-               "B.serial_rw_model": B.serial_rw_model(n * count * 4, count * 4, b["read"], copy_gbps, t, b["write"]),
+               "serial_rw_model": B.serial_rw_model(n * count * 4, count * 4, b["read"], copy_gbps, t, b["write"]),
                "sample_exact": ok}
         rows.append(row)
         print(json.dumps(row), flush=True)
     c3 = [r for r in rows if r["config"] == "C3"]
     print(json.dumps({"summary": "c3_vs_c2", "rounds": args.rounds, "steps": args.steps, "copy_GBps": round(copy_gbps, 1),
-                      "c2_GBps": rows[0]["GBps"], "c2_model_frac": (rows[0]["B.serial_rw_model"] or {}).get("frac_write_probe"),
+                      "c2_GBps": rows[0]["GBps"], "c2_model_frac": (rows[0]["serial_rw_model"] or {}).get("frac_write_probe"),
                       "c3_ratio_to_c2": {r["n"]: r["ratio_to_c2"] for r in c3},
-                      "c3_model_frac": {r["n"]: (r["B.serial_rw_model"] or {}).get("frac_write_probe") for r in c3},
+                      "c3_model_frac": {r["n"]: (r["serial_rw_model"] or {}).get("frac_write_probe") for r in c3},
                       "device": torch.cuda.get_device_properties(0).name}), flush=True)
     return 0
 
