@@ -1186,6 +1186,9 @@ constexpr int kDefBlock = 256;
 constexpr int kDefUnroll = 4;
 static_assert(kDefUnroll == 4, "default_grab / unit_sched_for default their unroll to 4");
 constexpr int kDefPol = 11;  // nt loads, nt stores
+// A launch that writes at most this many bytes stores write-through (system
+// scope, sc0 sc1) unless its config names a store form: see plan_store_peer.
+constexpr uint64_t kWtMaxBytes = 32ull << 20;
 constexpr int kDefBpc = 1;
 constexpr int kSmallBpc = 4;
 constexpr int kPhBlock = 512;
@@ -1353,6 +1356,7 @@ single_fn pick_nt(int pol) {
     case 11: return launch_single_t<Op, B, U, 11>;
     case 20: return launch_single_t<Op, B, U, 20>;
     case 21: return launch_single_t<Op, B, U, 21>;
+    case 10 * kPolStoreSys + 1: return launch_single_t<Op, B, U, 10 * kPolStoreSys + 1>;
     default: return nullptr;
   }
 }
@@ -1379,6 +1383,7 @@ single_fn pick_phase(const Cfg &c) {
   if (c.block == kPhBlock && c.unroll == PD) {
     switch (pol) {
       case 11: return launch_single_t<Op, kPhBlock, PD, 11, kPhase>;
+      case 10 * kPolStoreSys + 1: return launch_single_t<Op, kPhBlock, PD, 10 * kPolStoreSys + 1, kPhase>;
       case 1: if constexpr (TUNED) return launch_single_t<Op, kPhBlock, PD, 1, kPhase>; break;
       case 10: if constexpr (TUNED) return launch_single_t<Op, kPhBlock, PD, 10, kPhase>; break;
       case 21: if constexpr (TUNED) return launch_single_t<Op, kPhBlock, PD, 21, kPhase>; break;
@@ -1411,8 +1416,9 @@ single_fn pick_single(const Cfg &c) {
     if (c.block == 512) return pick_u<Op, 512>(c.unroll, pol);
     return nullptr;
   } else {
-    if (c.block != kDefBlock || c.unroll != kDefUnroll || pol != kDefPol) return nullptr;
-    return launch_single_t<Op, kDefBlock, kDefUnroll, kDefPol>;
+    if (c.block != kDefBlock || c.unroll != kDefUnroll) return nullptr;
+    if (pol == 10 * kPolStoreSys + 1) return launch_single_t<Op, kDefBlock, kDefUnroll, 10 * kPolStoreSys + 1>;
+    return pol == kDefPol ? launch_single_t<Op, kDefBlock, kDefUnroll, kDefPol> : nullptr;
   }
 }
 
@@ -1569,6 +1575,16 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
   const int dev = current_device();
   Split sp = split_on(out, count, esz);
   finish_cfg(c, sp.npkt, n, dtype, dev);
+  // the store form by size, as a plan's (plan_store_peer): write-through when
+  // the call writes at most kWtMaxBytes, its config leaves the store form
+  // open and its shape has a write-through kernel
+  if ((!cfg || cfg->store_policy == 0) && (uint64_t)count * esz <= kWtMaxBytes) {
+    Cfg w = c;
+    w.store = kPolStoreSys;
+    if (n > kMaxArgInputs ? pick_plan(dtype, w.acc, w.engine, w.unroll, plan_pol(HICCL_PEER_STORES)) != nullptr
+                          : pick_single_dtype(dtype, w) != nullptr)
+      c = w;
+  }
   if (c.bpc < 1 || c.bpc > 64) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: blocks_per_cu");
   if (c.grid < 0) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: grid < 0");
   if (n > kMaxArgInputs) {
@@ -1700,7 +1716,7 @@ namespace {
 // launch's output lines may sit dirty in the XCD L2s until the end-of-kernel
 // release writes them back, on the critical path of the next kernel on the
 // stream (MI355X_MICROARCH.md "boundary": + B / 6 TB/s for B dirty bytes).
-// So a plan that writes at most kPlanWtMaxBytes per launch stores with
+// So a plan that writes at most kWtMaxBytes per launch stores with
 // system-scope write-through (sc0 sc1, the peer-store form) instead, when its
 // config leaves the store form to size (store_policy 0).  Measured on the C5
 // step (4 x n = 2 + 1 x n = 4 computes of 2^18 f32, 5 MiB written, plus its
@@ -1708,9 +1724,8 @@ namespace {
 // profiles/r05d_step_store.jsonl): the reduction 4.52 -> 3.53 us per eager
 // launch (0.49 -> 0.63 of 8 TB/s), 3.01 -> 2.91 us under graph replay, the
 // copies 3.53 -> 3.28 us; 10-20 MiB written 20-38 % faster; at 80 MiB the
-// reduction still 3 % faster but the copies 4.5 % slower -- hence the cap.
-constexpr uint64_t kPlanWtMaxBytes = 32ull << 20;
-
+// reduction still 3 % faster but the copies 4.5 % slower -- hence the cap
+// (kWtMaxBytes; one-shot calls follow the same rule, hiccl_reduce_ex).
 int plan_store_peer(const hiccl_reduce_plan *p) {
   const int req = p->req.store_policy;  // 0: by size; 2: nt; 4: write-through (plan_set_config checked it)
   if (req == kPolStoreSys + 1) return HICCL_PEER_STORES;
@@ -1721,7 +1736,7 @@ int plan_store_peer(const hiccl_reduce_plan *p) {
   if (u && u != 2 && u != kDefUnroll && p->req.engine != HICCL_ENGINE_PHASE) return 0;
   uint64_t out = 0;
   for (auto &c : p->comps) out += (uint64_t)c.count * p->esz;
-  return out <= kPlanWtMaxBytes ? HICCL_PEER_STORES : 0;
+  return out <= kWtMaxBytes ? HICCL_PEER_STORES : 0;
 }
 
 int plan_eff_peer(const hiccl_reduce_plan *p) { return p->peer | plan_store_peer(p); }

@@ -136,9 +136,10 @@ typedef struct {
   int acc;           /* hiccl_acc_t */
   int grid;          /* total workgroups; overrides blocks_per_cu when > 0 */
   int store_policy;  /* stores: 1 plain, 2 nt, 3 sc1 (write-through, line dropped from L2),
-                        4 system-scope write-through (sc0 sc1; plans only).  0: nt for a
-                        one-shot call; for a plan, 4 when a launch writes at most 32 MiB
-                        (no dirty L2 lines left for the kernel boundary), else 2 */
+                        4 system-scope write-through (sc0 sc1).  0: 4 when the launch
+                        writes at most 32 MiB and its shape has a write-through kernel
+                        (TILE unroll 1 / 2 / 4, PHASE's default shape) -- no dirty L2
+                        lines left for the kernel boundary -- else 2 */
   int engine;        /* hiccl_engine_t */
   int schedule;      /* hiccl_schedule_t */
   int grab;          /* dynamic schedule: units per ticket (0 = default: PHASE 1,

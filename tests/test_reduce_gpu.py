@@ -960,6 +960,36 @@ def test_byte_copy_plan_small_is_write_through():
     comp.close()
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.uint16, np.float64, np.int32], ids=["f32", "bf16", "f64", "i32"])
+@pytest.mark.parametrize("cfg", [None, dict(store_policy=4), dict(store_policy=4, engine=2),
+                                 dict(store_policy=4, engine=1, unroll=2), dict(store_policy=2)],
+                         ids=["auto", "wt", "wt-phase", "wt-u2", "nt"])
+def test_oneshot_store_forms_same_bits(oracle, dtype, cfg):
+    """One-shot calls take the write-through store form by size too (the
+    default below 32 MiB written) or on request; misaligned output, same
+    bits as the oracle in every form the type has."""
+    if cfg and cfg.get("unroll") == 2 and np.dtype(dtype) not in (np.dtype(np.float32), np.dtype(np.uint16)):
+        pytest.skip("unroll 2 exists for f32 / bf16 only")
+    n, count = 5, 300007
+    x = oracle.fill(n, count, seed=4242, dtype=dtype)
+    tdt = TORCH_OF[np.dtype(dtype)]
+    ins = [to_dev(r).view(tdt) for r in x]
+    ob = torch.empty(count + 1, dtype=tdt, device=DEV)
+    hiccl_amd.reduce(ob[1:], ins, config=cfg)
+    torch.cuda.synchronize()
+    got = to_host(ob[1:], dtype)
+    e = oracle.reduce(list(x), dtype=dtype)
+    assert bits_equal(got, e), first_mismatch(got, e)
+
+
+def test_oneshot_write_through_needs_its_shape():
+    """Explicit write-through with a shape only the nt kernels have (wide
+    tiles) is refused, never silently replaced."""
+    x = [torch.zeros(1 << 16, device=DEV) for _ in range(2)]
+    with pytest.raises(hiccl_amd.HicclError):
+        hiccl_amd.reduce(torch.empty(1 << 16, device=DEV), x, config=dict(store_policy=4, engine=1, unroll=8))
+
+
 def test_plan_config_refuses_unsupported_fields():
     for bad in (dict(engine=1, unroll=32), dict(engine=1, unroll=3), dict(engine=2, unroll=4), dict(engine=1, block=512),
                 dict(nontemporal=1), dict(store_policy=3), dict(store_policy=1), dict(drain=1), dict(schedule=7)):

@@ -134,7 +134,42 @@ def main():
         for kind in ("red", "cp"):
             for p in (0, 1):
                 cases[f][kind][p].close()
+    oneshot()
     return 0
+
+
+def oneshot():
+    """One-shot hiccl_reduce calls (the single-compute kernel) of n inputs x
+    1-64 MiB: nt vs write-through stores (store_policy 2 / 4) and the default
+    (0: by size), queued, interleaved rounds; the same bits."""
+    stream = torch.cuda.current_stream()
+    rows = []
+    for n in (2, 8):
+        for mib in (1, 4, 16, 32, 64):
+            c = (mib << 20) // 4
+            ins = [torch.empty(c, device="cuda") for _ in range(n)]
+            for k, t in enumerate(ins):
+                hiccl_amd.fill_uniform(t, B.SEED, k)
+            outs = {k: torch.empty(c, device="cuda") for k in ("nt", "wt", "auto")}
+            cfgs = {"nt": dict(store_policy=2), "wt": dict(store_policy=4), "auto": None}
+            res = {k: [] for k in cfgs}
+            for _ in range(5):
+                for k, cfg in cfgs.items():
+                    res[k].append(B.time_queued(lambda: hiccl_amd.reduce(outs[k], ins, config=cfg, stream=stream),
+                                                100, 5) * 1e3)
+            torch.cuda.synchronize()
+            ok = all(torch.equal(outs["nt"].view(torch.int32), outs[k].view(torch.int32)) for k in ("wt", "auto"))
+            nb = (n + 1) * c * 4
+            row = {"mode": "oneshot_store", "n": n, "mib_per_input": mib, "bits_ok": bool(ok)}
+            for k in cfgs:
+                t = float(np.median(res[k]))
+                row[f"{k}_us"] = round(t, 3)
+                row[f"{k}_GBps"] = round(nb / t * 1e-3, 1)
+            row["wt_over_nt"] = round(row["wt_us"] / row["nt_us"], 4)
+            rows.append(row)
+            print(json.dumps(row), flush=True)
+            del ins, outs
+    return rows
 
 
 if __name__ == "__main__":
