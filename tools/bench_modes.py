@@ -309,7 +309,7 @@ def progstep(args):
     # The same steps captured into one hipGraph of 200 steps and replayed, as
     # HICCL_GRAPH=1 runs a pipeline: every phase's epoch is e + *ctr, ctr
     # bumped by the graph's first node (a kernel boundary between graph
-    # nodes costs less than between eager launches: bench --stepscale).
+    # nodes costs less than between eager launches: tools/archive/bench_probes.py --mode stepscale).
     ctr = torch.zeros(1, dtype=torch.int32, device="cuda")
     cptr = ctypes.c_void_p(ctr.data_ptr())
     erp = ctypes.c_void_p(err.data_ptr())
