@@ -45,7 +45,7 @@ ABI_LINK = -Lhiccl_amd -lhiccl_reduce -Wl,-rpath,'$$ORIGIN/../hiccl_amd' -L/opt/
 HDRS = include/hiccl.h $(wildcard include/hiccl/*.h) include/hiccl_reduce.h hiccl_amd/csrc/compose.h
 
 CPP_BINS = build/plan_dump build/collectives_host build/collectives_host_f32 build/collectives_hip build/collectives_hip_f32 \
-           build/readme_example_host build/readme_example_hip build/abi_c build/ipc_reuse
+           build/readme_example_host build/readme_example_hip build/abi_c build/ipc_reuse build/sync_wait_probe
 
 cpp: $(CPP_BINS)
 
@@ -81,6 +81,11 @@ build/readme_example_hip: hiccl_amd/csrc/readme_example.cpp $(HDRS) $(LIB)
 build/ipc_reuse: tests/cpp/ipc_reuse.cpp include/hiccl_reduce.h $(LIB)
 	@mkdir -p build
 	$(CXX) $(CXXFLAGS) -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o $@ $< $(ABI_LINK) $(MPI_LINK)
+
+# host wait after a C5-step launch, from C++ (tools/sync_wait_probe.cpp)
+build/sync_wait_probe: tools/sync_wait_probe.cpp include/hiccl_reduce.h $(LIB)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o $@ $< $(ABI_LINK)
 
 # plain C99 client of the C ABI (the header must stay C)
 build/abi_c: tests/cpp/abi_c.c include/hiccl_reduce.h $(LIB)
