@@ -81,6 +81,7 @@ def test_invalid_arguments_rejected_on_host():
     assert lib.hiccl_reduce_plan_set_peer(None, L.HICCL_PEER_STORES) == 1
     assert "plan is NULL" in L.last_error()
     assert lib.hiccl_reduce_plan_peer(None) == -1
+    assert lib.hiccl_reduce_plan_store_policy(None) == -1
     assert lib.hiccl_reduce_plan_numcomp(None) == 0
     lib.hiccl_reduce_plan_destroy(None)
     # host pipe: argument checks come before any HIP call
