@@ -123,20 +123,22 @@ def numa_locality(bufs, thread_cpus, per_block=32):
     local fraction and the page count per node, or None if the query fails."""
     libc = ctypes.CDLL(None, use_errno=True)
     T = len(thread_cpus)
+    nodes = [cpu_node(c) for c in thread_cpus]
     addrs, want = [], []
     for b in bufs:
         count, base = b.size, b.ctypes.data
         q, r = divmod(count, T)
-        for t, c in enumerate(thread_cpus):
+        for t in range(T):
             lo = q * t + min(t, r)
             hi = lo + q + (1 if t < r else 0)
             for j in range(per_block):
                 i = lo + (hi - lo) * j // per_block
-                addrs.append((base + 4 * i) & ~4095)
-                want.append(cpu_node(c))
+                addrs.append((base + b.itemsize * i) & ~4095)
+                want.append(nodes[t])
     n = len(addrs)
     pages = (ctypes.c_void_p * n)(*addrs)
     status = (ctypes.c_int * n)()
+    # move_pages(2) (x86_64 syscall 279) with nodes == NULL: a query, nothing moves
     rc = libc.syscall(ctypes.c_long(279), ctypes.c_int(0), ctypes.c_ulong(n), pages, None, status, ctypes.c_int(0))
     if rc != 0:
         return None
