@@ -610,8 +610,9 @@ class Comm {
     return std::max(8, cus / device_ranks);
   }
 
-  // Default: OFF (hiccl_step_program_default(); HICCL_STEP_PROGRAM=1 opts
-  // in), whatever the device layout.  Programs were measured only with ranks
+  // Default: OFF (hiccl_step_program_default(); HICCL_STEP_PROGRAM=1, yes,
+  // on or true opts in, any other value stays off and is named on stderr),
+  // whatever the device layout.  Programs were measured only with ranks
   // sharing one GPU, where they lose (a program's workgroups wait on the
   // device for the peer's token while the peer's kernels need that device to
   // produce it: 2 ranks, pipedepth 128, 64 MiB/rank, graph + fused 2.67-2.93
