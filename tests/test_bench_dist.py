@@ -406,3 +406,14 @@ def test_driver_line_stays_compact():
     assert out["c5"]["stopped_after"] == "xccl" and out["c5"]["xccl"]["rc"] == 124
     assert out["c5"]["host"]["kat"] == "PASSED" and "host_split_us_per_step" not in out["c5"]["host"]
     assert out["c5"]["protocol_ab"]["baseline_ms"] == 31.5
+
+
+def test_compact_c5_skipped_leg():
+    """A leg skipped as a whole (fewer GPUs than ranks, an error) keeps its
+    reason and the mask scrub drops out of the driver's line."""
+    sys.path.insert(0, ROOT)
+    import bench
+    out = bench.compact_c5({"skipped": "2 ranks on 1 GPU(s): config 5 needs one GPU per rank",
+                            "env_scrubbed": {"HIP_VISIBLE_DEVICES": "0"}, "devices_counted_unmasked": 1})
+    assert out == {"skipped": "2 ranks on 1 GPU(s): config 5 needs one GPU per rank"}
+    assert bench.compact_c5({"skipped": "error: boom"}) == {"skipped": "error: boom"}
