@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Where does write-through stop paying?  Round 5 stores write-through when a
+launch writes <= 32 MiB (kWtMaxBytes), set from the C5 step shape scaled
+1/4x-16x (tools/step_store_probe.py: reductions still 3-6 % faster at 40
+and 80 MiB written, byte copies 4-5 % slower at 80 MiB).  This probe times
+larger launches with both store forms (store_policy 2 nt / 4 write-through),
+interleaved rounds, events around each launch (median), same bits:
+  * one-shot reductions of 8 inputs writing 32 / 64 / 128 / 256 MiB
+    (C4's 64 MiB-per-input bucket is the 64 MiB row; C3 n = 8 the 256 MiB);
+  * the same buckets as plans of 1 MiB computes (C4's structure);
+  * one-shot reductions of 2 inputs writing 64 / 256 MiB (few inputs: the
+    write share is a third of the bytes);
+  * byte copies of 48 / 64 / 128 MiB (the transport's).
+One JSON line per case.
+
+    python tools/store_threshold_probe.py > gpurun_out/<tag>_store_threshold.jsonl
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench as B  # noqa: E402
+import hiccl_amd  # noqa: E402
+
+FORMS = {"nt": 2, "wt": 4}
+
+
+def timed(fns, steps=10, warmup=3, rounds=5):
+    res = {k: [] for k in fns}
+    for _ in range(rounds):
+        for k, fn in fns.items():
+            _, ms = B.time_launches(fn, steps, warmup)
+            res[k].append(float(np.median(ms)))
+    return {k: float(np.median(v)) for k, v in res.items()}
+
+
+def row(kind, n, mib, nbytes, t, ok, extra=None):
+    r = {"mode": "store_threshold", "kind": kind, "n": n, "mib_written": mib, "bits_ok": bool(ok)}
+    for k, v in t.items():
+        r[f"{k}_us"] = round(v * 1e3, 2)
+        r[f"{k}_GBps"] = round(nbytes / (v * 1e-3) / 1e9, 1)
+    r["wt_over_nt"] = round(t["wt"] / t["nt"], 4)
+    r.update(extra or {})
+    print(json.dumps(r), flush=True)
+
+
+def main():
+    stream = torch.cuda.current_stream()
+    for n, mibs in ((8, (32, 64, 128, 256)), (2, (64, 256))):
+        for mib in mibs:
+            c = (mib << 20) // 4
+            ins = [torch.empty(c, device="cuda") for _ in range(n)]
+            for k, t in enumerate(ins):
+                hiccl_amd.fill_uniform(t, B.SEED, k)
+            outs = {f: torch.empty(c, device="cuda") for f in FORMS}
+            fns = {f: (lambda f=f: hiccl_amd.reduce(outs[f], ins, config=dict(store_policy=FORMS[f]),
+                                                    stream=stream)) for f in FORMS}
+            t = timed(fns)
+            torch.cuda.synchronize()
+            ok = torch.equal(outs["nt"].view(torch.int32), outs["wt"].view(torch.int32))
+            row("oneshot", n, mib, (n + 1) * c * 4, t, ok)
+            if n == 8:
+                plans = {}
+                for f in FORMS:
+                    comp = hiccl_amd.Compute(torch.float32, device=torch.cuda.current_device(),
+                                             config=dict(store_policy=FORMS[f]))
+                    step = (1 << 20) // 4
+                    for off in range(0, c, step):
+                        comp.add([(x, off) for x in ins], (outs[f], off), min(step, c - off), compid=0)
+                    plans[f] = comp
+                t = timed({f: (lambda p=p: p.start(stream=stream)) for f, p in plans.items()})
+                torch.cuda.synchronize()
+                ok = torch.equal(outs["nt"].view(torch.int32), outs["wt"].view(torch.int32))
+                row("plan_1MiB_computes", n, mib, (n + 1) * c * 4, t, ok,
+                    {"engine": plans["nt"].engine(), "computes": mib})
+                for p in plans.values():
+                    p.close()
+            del ins, outs
+            torch.cuda.empty_cache()
+    for mib in (48, 64, 128):
+        nb = mib << 20
+        src = torch.randint(0, 256, (nb,), dtype=torch.uint8, device="cuda")
+        dst = {f: torch.empty(nb, dtype=torch.uint8, device="cuda") for f in FORMS}
+        fns = {f: (lambda f=f: hiccl_amd.reduce(dst[f], [src], config=dict(store_policy=FORMS[f]), stream=stream))
+               for f in FORMS}
+        t = timed(fns)
+        torch.cuda.synchronize()
+        ok = all(torch.equal(d, src) for d in dst.values())
+        row("byte_copy", 1, mib, 2 * nb, t, ok)
+        del src, dst
+        torch.cuda.empty_cache()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
