@@ -50,8 +50,29 @@ def row(kind, n, mib, nbytes, t, ok, extra=None):
     print(json.dumps(r), flush=True)
 
 
+def c3(stream):
+    """Config 3's buckets (n x 256 MiB, 256 MiB written) in both forms."""
+    c = (256 << 20) // 4
+    for n in (2, 3, 4, 8, 16, 32, 64):
+        ins = [torch.empty(c, device="cuda") for _ in range(n)]
+        for k, t in enumerate(ins):
+            hiccl_amd.fill_uniform(t, B.SEED, k)
+        outs = {f: torch.empty(c, device="cuda") for f in FORMS}
+        fns = {f: (lambda f=f: hiccl_amd.reduce(outs[f], ins, config=dict(store_policy=FORMS[f]), stream=stream))
+               for f in FORMS}
+        t = timed(fns)
+        torch.cuda.synchronize()
+        ok = torch.equal(outs["nt"].view(torch.int32), outs["wt"].view(torch.int32))
+        row("c3_oneshot", n, 256, (n + 1) * c * 4, t, ok)
+        del ins, outs
+        torch.cuda.empty_cache()
+
+
 def main():
     stream = torch.cuda.current_stream()
+    if len(sys.argv) > 1 and sys.argv[1] == "c3":
+        c3(stream)
+        return 0
     for n, mibs in ((8, (32, 64, 128, 256)), (2, (64, 256))):
         for mib in mibs:
             c = (mib << 20) // 4
