@@ -68,10 +68,44 @@ def c3(stream):
         torch.cuda.empty_cache()
 
 
+def big(stream):
+    """Config 2's bucket (8 x 1 GiB) and 2 x 1 GiB / 8 x 512 MiB: AUTO (TILE
+    on the dynamic schedule at C2) and the phased engine, each with nt and
+    write-through stores; wide tiles (AUTO at 2 x 1 GiB) have nt only."""
+    for n, mib in ((8, 1024), (8, 512), (2, 1024)):
+        c = (mib << 20) // 4
+        ins = [torch.empty(c, device="cuda") for _ in range(n)]
+        for k, t in enumerate(ins):
+            hiccl_amd.fill_uniform(t, B.SEED, k)
+        out = {}
+        variants = {"auto_nt": dict(store_policy=2), "phase_nt": dict(store_policy=2, engine=2),
+                    "phase_wt": dict(store_policy=4, engine=2), "tile4_nt": dict(store_policy=2, engine=1, unroll=4),
+                    "tile4_wt": dict(store_policy=4, engine=1, unroll=4)}
+        if n == 8:
+            variants["auto_wt"] = dict(store_policy=4)
+        for k in variants:
+            out[k] = torch.empty(c, device="cuda")
+        fns = {k: (lambda k=k: hiccl_amd.reduce(out[k], ins, config=variants[k], stream=stream)) for k in variants}
+        t = timed(fns, steps=10, warmup=2, rounds=5)
+        torch.cuda.synchronize()
+        ok = all(torch.equal(out["auto_nt"].view(torch.int32), v.view(torch.int32)) for v in out.values())
+        nb = (n + 1) * c * 4
+        r = {"mode": "store_threshold", "kind": "big", "n": n, "mib_written": mib, "bits_ok": bool(ok)}
+        for k, v in t.items():
+            r[f"{k}_ms"] = round(v, 4)
+            r[f"{k}_frac"] = round(nb / (v * 1e-3) / 1e9 / 8000.0, 4)
+        print(json.dumps(r), flush=True)
+        del ins, out
+        torch.cuda.empty_cache()
+
+
 def main():
     stream = torch.cuda.current_stream()
     if len(sys.argv) > 1 and sys.argv[1] == "c3":
         c3(stream)
+        return 0
+    if len(sys.argv) > 1 and sys.argv[1] == "big":
+        big(stream)
         return 0
     for n, mibs in ((8, (32, 64, 128, 256)), (2, (64, 256))):
         for mib in mibs:
