@@ -1188,7 +1188,11 @@ static_assert(kDefUnroll == 4, "default_grab / unit_sched_for default their unro
 constexpr int kDefPol = 11;  // nt loads, nt stores
 // A launch that writes at most this many bytes stores write-through (system
 // scope, sc0 sc1) unless its config names a store form: see plan_store_peer.
+// Copies (one input) up to 32 MiB; reductions (two or more inputs per
+// output, packet-weighted for a plan) up to 256 MiB.
 constexpr uint64_t kWtMaxBytes = 32ull << 20;
+constexpr uint64_t kWtMaxBytesReduce = 256ull << 20;
+inline uint64_t wt_cap(double n) { return n >= 1.5 ? kWtMaxBytesReduce : kWtMaxBytes; }
 constexpr int kDefBpc = 1;
 constexpr int kSmallBpc = 4;
 constexpr int kPhBlock = 512;
@@ -1576,9 +1580,9 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
   Split sp = split_on(out, count, esz);
   finish_cfg(c, sp.npkt, n, dtype, dev);
   // the store form by size, as a plan's (plan_store_peer): write-through when
-  // the call writes at most kWtMaxBytes, its config leaves the store form
+  // the call writes at most wt_cap(n) bytes, its config leaves the store form
   // open and its shape has a write-through kernel
-  if ((!cfg || cfg->store_policy == 0) && (uint64_t)count * esz <= kWtMaxBytes) {
+  if ((!cfg || cfg->store_policy == 0) && (uint64_t)count * esz <= wt_cap(dtype == HICCL_BYTES ? 1.0 : n)) {
     Cfg w = c;
     w.store = kPolStoreSys;
     if (n > kMaxArgInputs ? pick_plan(dtype, w.acc, w.engine, w.unroll, plan_pol(HICCL_PEER_STORES)) != nullptr
@@ -1716,16 +1720,21 @@ namespace {
 // launch's output lines may sit dirty in the XCD L2s until the end-of-kernel
 // release writes them back, on the critical path of the next kernel on the
 // stream (MI355X_MICROARCH.md "boundary": + B / 6 TB/s for B dirty bytes).
-// So a plan that writes at most kWtMaxBytes per launch stores with
+// So a plan that writes at most wt_cap(n) bytes per launch stores with
 // system-scope write-through (sc0 sc1, the peer-store form) instead, when its
 // config leaves the store form to size (store_policy 0).  Measured on the C5
 // step (4 x n = 2 + 1 x n = 4 computes of 2^18 f32, 5 MiB written, plus its
 // five 1 MiB byte copies; tools/step_store_probe.py,
 // profiles/r05d_step_store.jsonl): the reduction 4.52 -> 3.53 us per eager
 // launch (0.49 -> 0.63 of 8 TB/s), 3.01 -> 2.91 us under graph replay, the
-// copies 3.53 -> 3.28 us; 10-20 MiB written 20-38 % faster; at 80 MiB the
-// reduction still 3 % faster but the copies 4.5 % slower -- hence the cap
-// (kWtMaxBytes; one-shot calls follow the same rule, hiccl_reduce_ex).
+// copies 3.53 -> 3.28 us; 10-20 MiB written 20-38 % faster.  Byte copies
+// lose from 48 MiB written (1-4 %); reductions keep gaining up to 256 MiB
+// (tools/store_threshold_probe.py: 8 inputs writing 32-256 MiB 1.6-3 %
+// faster, config 3's buckets -- n x 256 MiB -- 1.2-9.2 %, n = 2 reaching
+// 7.02 TB/s; profiles/r05o_store_threshold.jsonl, r05p_store_c3.jsonl) and
+// stop at 512 MiB and 1 GiB (-0.7 / -0.6 % on the TILE engine, config 2 no
+// gain; r05q_store_big.jsonl, r05j_c2_store_ab.jsonl): hence the two caps
+// (wt_cap; one-shot calls follow the same rule, hiccl_reduce_ex).
 int plan_store_peer(const hiccl_reduce_plan *p) {
   const int req = p->req.store_policy;  // 0: by size; 2: nt; 4: write-through (plan_set_config checked it)
   if (req == kPolStoreSys + 1) return HICCL_PEER_STORES;
@@ -1735,8 +1744,13 @@ int plan_store_peer(const hiccl_reduce_plan *p) {
   const int u = p->req.unroll;
   if (u && u != 2 && u != kDefUnroll && p->req.engine != HICCL_ENGINE_PHASE) return 0;
   uint64_t out = 0;
-  for (auto &c : p->comps) out += (uint64_t)c.count * p->esz;
-  return out <= kWtMaxBytes ? HICCL_PEER_STORES : 0;
+  double weighted_n = 0;
+  for (auto &c : p->comps) {
+    out += (uint64_t)c.count * p->esz;
+    weighted_n += (double)c.count * (double)c.in.size();
+  }
+  const double n = out ? weighted_n * (double)p->esz / (double)out : 0.0;
+  return out <= wt_cap(p->dtype == HICCL_BYTES ? 1.0 : n) ? HICCL_PEER_STORES : 0;
 }
 
 int plan_eff_peer(const hiccl_reduce_plan *p) { return p->peer | plan_store_peer(p); }

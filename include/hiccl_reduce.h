@@ -137,9 +137,10 @@ typedef struct {
   int grid;          /* total workgroups; overrides blocks_per_cu when > 0 */
   int store_policy;  /* stores: 1 plain, 2 nt, 3 sc1 (write-through, line dropped from L2),
                         4 system-scope write-through (sc0 sc1).  0: 4 when the launch
-                        writes at most 32 MiB and its shape has a write-through kernel
-                        (TILE unroll 1 / 2 / 4, PHASE's default shape) -- no dirty L2
-                        lines left for the kernel boundary -- else 2 */
+                        writes at most 256 MiB of sums (two or more inputs) or 32 MiB
+                        of copies (one input) and its shape has a write-through
+                        kernel (TILE unroll 1 / 2 / 4, PHASE's default shape) -- no
+                        dirty L2 lines left for the kernel boundary -- else 2 */
   int engine;        /* hiccl_engine_t */
   int schedule;      /* hiccl_schedule_t */
   int grab;          /* dynamic schedule: units per ticket (0 = default: PHASE 1,
@@ -198,9 +199,10 @@ int hiccl_reduce_plan_set_engine(hiccl_reduce_plan_t *plan, int engine);
  * blocks_per_cu, grid, acc, and the TILE shape block 256 x unroll 4 (f32 and
  * bf16 also unroll 1, 2, 8 or 16); PHASE runs its default shape; loads are
  * nt; stores are nt (store_policy 2), system-scope write-through (4), or
- * (0, the default) write-through when a launch writes at most 32 MiB and nt
- * above -- the pipeline-step sizes, where nt lines left dirty in the L2s
- * cost the kernel boundary their write-back -- except
+ * (0, the default) write-through when a launch writes at most 256 MiB of
+ * sums or 32 MiB of byte copies and nt above -- pipeline steps and mid-size
+ * buckets, where nt lines left dirty in the L2s cost the kernel boundary
+ * their write-back -- except
  * for an explicit TILE unroll 1, 8 or 16, which stays nt.  Write-through
  * runs the shapes the peer kernels have (below).  Anything else is refused
  * with hipErrorInvalidValue -- no field is silently ignored. */

@@ -923,12 +923,14 @@ def test_plan_store_form_small_step(oracle, cfg, want):
     comp.close()
 
 
-@pytest.mark.parametrize("cfg,want", [(None, 2), (dict(store_policy=4), 4)], ids=["auto-nt", "wt"])
-def test_plan_store_form_large(oracle, cfg, want):
-    """Above 32 MiB written per launch the default is nt (at 80 MiB the
-    step's byte copies ran 4.5 % slower write-through); write-through on
-    request; sampled-exact at 8 inputs x 64 MiB in 1 MiB computes."""
-    n, count, seed = 8, 1 << 24, 808
+@pytest.mark.parametrize("log2count,cfg,want", [(24, None, 4), (27, None, 2), (27, dict(store_policy=4), 4)],
+                         ids=["64MiB-auto-wt", "512MiB-auto-nt", "512MiB-wt"])
+def test_plan_store_form_large(oracle, log2count, cfg, want):
+    """A reduction plan writing up to 256 MiB per launch stores write-through
+    by default (config 3 / 4 sizes: 1.6-9 % faster), above it nt (512 MiB
+    and 1 GiB: no gain); write-through on request; sampled-exact at 8 inputs
+    in 1 MiB computes."""
+    n, count, seed = 8, 1 << log2count, 808
     ins = [torch.empty(count, device=DEV) for _ in range(n)]
     for k, t in enumerate(ins):
         hiccl_amd.fill_uniform(t, seed, k)
@@ -945,9 +947,25 @@ def test_plan_store_form_large(oracle, cfg, want):
     comp.close()
 
 
-def test_byte_copy_plan_small_is_write_through():
+def test_byte_copy_plan_store_forms():
+    """Byte copies (the transport's, HICCL_BYTES plans) store write-through
+    up to 32 MiB per launch and nt above (they lose from 48 MiB written),
+    exact."""
+    big = hiccl_amd.Compute(torch.uint8, device=0)
+    src = torch.randint(0, 256, (48 << 20,), dtype=torch.uint8, device=DEV)
+    dst = torch.zeros(48 << 20, dtype=torch.uint8, device=DEV)
+    big.add([src], dst, 48 << 20, compid=0)
+    assert big.store_policy() == 2
+    big.start()
+    big.wait()
+    assert torch.equal(src, dst)
+    big.close()
+    _byte_copy_plan_small()
+
+
+def _byte_copy_plan_small():
     """The transport's per-step copies (HICCL_BYTES plans, 1 MiB each) take
-    the write-through form too, exact."""
+    the write-through form, exact."""
     comp = hiccl_amd.Compute(torch.uint8, device=0)
     src = [torch.randint(0, 256, ((1 << 20) + 3,), dtype=torch.uint8, device=DEV) for _ in range(5)]
     dst = [torch.zeros((1 << 20) + 3, dtype=torch.uint8, device=DEV) for _ in range(5)]
