@@ -99,8 +99,47 @@ def big(stream):
         torch.cuda.empty_cache()
 
 
+def split(stream):
+    """Config 2's bucket (8 x 1 GiB, one set of allocations) reduced by one
+    launch, or by 2 / 4 / 8 launches over consecutive element ranges (views
+    of the same buffers), each in its default store form (a quarter or an
+    eighth writes <= 256 MiB: write-through) and the quarters also nt;
+    whole-bucket time between events around the launches, interleaved
+    rounds, same bits."""
+    n, c = 8, 1 << 28
+    ins = [torch.empty(c, device="cuda") for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, B.SEED, k)
+    outs = {}
+
+    def parts(k, cfg=None):
+        out = outs.setdefault((k, str(cfg)), torch.empty(c, device="cuda"))
+        step = c // k
+
+        def run():
+            for j in range(k):
+                lo = j * step
+                hiccl_amd.reduce(out[lo:lo + step], [x[lo:lo + step] for x in ins], config=cfg, stream=stream)
+        return run
+    fns = {"one": parts(1), "halves": parts(2), "quarters": parts(4), "quarters_nt": parts(4, dict(store_policy=2)),
+           "eighths": parts(8)}
+    t = timed(fns, steps=10, warmup=2, rounds=5)
+    torch.cuda.synchronize()
+    ref = outs[(1, "None")]
+    ok = all(torch.equal(ref.view(torch.int32), v.view(torch.int32)) for v in outs.values())
+    nb = (n + 1) * c * 4
+    r = {"mode": "store_threshold", "kind": "c2_split", "bits_ok": bool(ok)}
+    for k, v in t.items():
+        r[f"{k}_ms"] = round(v, 4)
+        r[f"{k}_frac"] = round(nb / (v * 1e-3) / 1e9 / 8000.0, 4)
+    print(json.dumps(r), flush=True)
+
+
 def main():
     stream = torch.cuda.current_stream()
+    if len(sys.argv) > 1 and sys.argv[1] == "split":
+        split(stream)
+        return 0
     if len(sys.argv) > 1 and sys.argv[1] == "c3":
         c3(stream)
         return 0
