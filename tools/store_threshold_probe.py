@@ -135,8 +135,37 @@ def split(stream):
     print(json.dumps(r), flush=True)
 
 
+def engines(stream):
+    """Config 3's few-input buckets (n x 256 MiB) with the round-5 default
+    store form (write-through at this size): AUTO against the TILE engine
+    (static and dynamic) and the phased engine, interleaved rounds -- does
+    AUTO's engine choice, set with nt stores, still hold?"""
+    c = (256 << 20) // 4
+    variants = {"auto": None, "tile": dict(engine=1), "tile_dyn": dict(engine=1, schedule=2),
+                "phase": dict(engine=2)}
+    for n in (2, 3, 4, 8):
+        ins = [torch.empty(c, device="cuda") for _ in range(n)]
+        for k, t in enumerate(ins):
+            hiccl_amd.fill_uniform(t, B.SEED, k)
+        outs = {v: torch.empty(c, device="cuda") for v in variants}
+        fns = {v: (lambda v=v: hiccl_amd.reduce(outs[v], ins, config=variants[v], stream=stream)) for v in variants}
+        t = timed(fns)
+        torch.cuda.synchronize()
+        ok = all(torch.equal(outs["auto"].view(torch.int32), o.view(torch.int32)) for o in outs.values())
+        nb = (n + 1) * c * 4
+        r = {"mode": "store_threshold", "kind": "c3_engines", "n": n, "bits_ok": bool(ok)}
+        for k, v in t.items():
+            r[f"{k}_GBps"] = round(nb / (v * 1e-3) / 1e9, 1)
+        print(json.dumps(r), flush=True)
+        del ins, outs
+        torch.cuda.empty_cache()
+
+
 def main():
     stream = torch.cuda.current_stream()
+    if len(sys.argv) > 1 and sys.argv[1] == "engines":
+        engines(stream)
+        return 0
     if len(sys.argv) > 1 and sys.argv[1] == "split":
         split(stream)
         return 0
