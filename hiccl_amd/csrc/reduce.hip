@@ -1217,11 +1217,12 @@ int phase_p_dtype(int dtype, int acc) {
 
 struct Cfg {
   int block, unroll, bpc, nt, acc, grid, store, engine, schedule, grab, drain;
+  bool store_auto;  // store_policy 0: the store form follows the launch's size (wt_cap)
 };
 
 // Raw config: zero block/unroll stay zero until the engine is known.
 Cfg resolve(const hiccl_reduce_config_t *c) {
-  Cfg r{0, 0, 0, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO, HICCL_SCHED_AUTO, 0, 0};
+  Cfg r{0, 0, 0, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO, HICCL_SCHED_AUTO, 0, 0, true};
   if (c) {
     r.block = c->block;
     r.unroll = c->unroll;
@@ -1230,6 +1231,7 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
     r.acc = c->acc;
     r.grid = c->grid;
     if (c->store_policy) r.store = c->store_policy - 1;
+    r.store_auto = c->store_policy == 0;
     r.engine = c->engine;
     r.schedule = c->schedule;
     r.grab = c->grab;
@@ -1289,6 +1291,13 @@ int auto_engine(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
   const uint64_t chunks = (npkt + chunk - 1) / chunk;
   const double round_eff = chunks ? (double)chunks / (double)(((chunks + cus - 1) / cus) * cus) : 0.0;
   if (n < 2.5) return per_cu > 16 && round_eff >= 0.89 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
+  // Round 5: with the write-through stores a launch of this size takes
+  // (store form left to size, at most wt_cap written; f32), static tiles lead
+  // the phased engine at three inputs: 6.80 vs 6.62 TB/s interleaved at
+  // 3 x 256 MiB (profiles/r05v_c3_engines.jsonl; 6.86 vs 6.63 on another
+  // box, r05r_nway.jsonl); at two and four inputs the nt table holds.
+  if (n >= 2.5 && n < 3.5 && c.store_auto && dtype == HICCL_FLOAT32 && npkt * kPacket <= wt_cap(n))
+    return HICCL_ENGINE_TILE;
   if (n < kDynMinInputs) return per_cu >= 4 && round_eff >= 0.89 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
   // many inputs, under the dynamic tiles' ticket count: PHASE from one
   // whole chunk per CU unless too much of the last round idles (f32 n = 8 at

@@ -153,8 +153,9 @@ def test_auto_choice_rule_table_on_host():
     cases = [  # (dtype, elements per input, n) -> (engine, unroll, blocks per CU, dynamic)
         ((f32, 1 << 28, 8), (T, 4, 1, 1)),       # C2: tiles on the ticket counter
         ((f32, 1 << 26, 2), (T, 4, 1, 0)),       # C3, two inputs: static tiles
-        ((f32, 1 << 26, 3), (P, 16, 1, 0)),      # C3, 3-4 inputs: 8 whole chunks per CU
-        ((f32, 1 << 26, 4), (P, 16, 1, 0)),
+        ((f32, 1 << 26, 3), (T, 4, 1, 0)),       # C3, 3 inputs, write-through (round 5): static tiles
+        ((f32, 1 << 26, 4), (P, 16, 1, 0)),      # C3, 4 inputs: 8 whole chunks per CU
+        ((f32, 1 << 27, 3), (P, 16, 1, 0)),      # 512 MiB written (nt): the phased engine
         ((f32, 1 << 26, 8), (T, 4, 1, 1)),       # C3, many inputs: 64 tickets per workgroup
         ((f32, 1 << 26, 64), (T, 4, 1, 1)),
         ((f32, 1 << 28, 2), (T, 16, 1, 1)),      # 1 GiB per input, few inputs: wide tiles
