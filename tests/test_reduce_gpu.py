@@ -398,7 +398,9 @@ def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
     a 128 KiB chunk (2^23 f32 per input) and the last round of chunks keeps
     >= 70 % of the CUs busy (n = 8 at 1.25 chunks per CU: TILE); with 3-4
     inputs PHASE from 4 chunks per CU in whole-enough rounds (~90 %),
-    with 2 inputs from 16; TILE otherwise."""
+    with 2 inputs from 16; TILE otherwise.  Round 5: three f32 inputs take
+    static tiles when the launch stores write-through (its store form left
+    to size, <= 256 MiB written); with nt stores asked for, the table above."""
     count = 1 << 23
     a = torch.empty(1 << 27, device=DEV)
     hiccl_amd.fill_uniform(a, 77, 0)
@@ -406,9 +408,10 @@ def test_plan_auto_engine_picks_phase_for_large_buckets(oracle):
     P, T = hiccl_amd.HICCL_ENGINE_PHASE, hiccl_amd.HICCL_ENGINE_TILE
     for cnt, n, expect in ((1 << 27, 6, T), (1 << 26, 6, P), (count, 6, P), (count, 2, T), (1 << 24, 2, T),
                            (1 << 26, 4, P), (count // 4, 6, T), (count // 4, 2, T), (count, 4, T),
-                           (count * 5 // 4, 8, T), (count * 3 // 2, 8, P), (count * 9 // 2, 3, P),
-                           (count * 5 // 2, 4, T)):
-        comp = hiccl_amd.Compute(torch.float32, device=0)
+                           (count * 5 // 4, 8, T), (count * 3 // 2, 8, P), (count * 9 // 2, 3, T),
+                           (count * 5 // 2, 4, T), (count * 9 // 2, 3, (P, dict(store_policy=2)))):
+        expect, cfg = expect if isinstance(expect, tuple) else (expect, None)
+        comp = hiccl_amd.Compute(torch.float32, device=0, config=cfg)
         comp.add([a] * n, out, cnt, compid=0)
         comp.start()
         comp.wait()
