@@ -161,8 +161,42 @@ def engines(stream):
         torch.cuda.empty_cache()
 
 
+def c4(stream):
+    """Config 4's batched plans (8 inputs in 1 MiB computes, one launch) at
+    16 / 64 / 256 MiB per input, f32 and bf16, nt against write-through,
+    interleaved rounds, same bits."""
+    for dtype in (torch.float32, torch.bfloat16):
+        esz = torch.tensor([], dtype=dtype).element_size()
+        for mib in (16, 64, 256):
+            c = (mib << 20) // esz
+            ins = [torch.empty(c, dtype=dtype, device="cuda") for _ in range(8)]
+            for k, t in enumerate(ins):
+                hiccl_amd.fill_uniform(t, B.SEED, k)
+            outs = {f: torch.empty(c, dtype=dtype, device="cuda") for f in FORMS}
+            plans = {}
+            step = (1 << 20) // esz
+            for f in FORMS:
+                comp = hiccl_amd.Compute(dtype, device=torch.cuda.current_device(), config=dict(store_policy=FORMS[f]))
+                for off in range(0, c, step):
+                    comp.add([(x, off) for x in ins], (outs[f], off), min(step, c - off), compid=0)
+                plans[f] = comp
+            t = timed({f: (lambda p=p: p.start(stream=stream)) for f, p in plans.items()})
+            torch.cuda.synchronize()
+            bits = torch.int16 if dtype == torch.bfloat16 else torch.int32
+            ok = torch.equal(outs["nt"].view(bits), outs["wt"].view(bits))
+            row("c4_plan", 8, mib, 9 * c * esz, t, ok, {"dtype": str(dtype).split(".")[-1],
+                                                         "engine": plans["nt"].engine()})
+            for p in plans.values():
+                p.close()
+            del ins, outs
+            torch.cuda.empty_cache()
+
+
 def main():
     stream = torch.cuda.current_stream()
+    if len(sys.argv) > 1 and sys.argv[1] == "c4":
+        c4(stream)
+        return 0
     if len(sys.argv) > 1 and sys.argv[1] == "engines":
         engines(stream)
         return 0
