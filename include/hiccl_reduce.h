@@ -153,7 +153,8 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
 
 /* What AUTO (engine, TILE unroll / PHASE packets per lane, workgroups per
  * CU, dynamic unit schedule 1/0) picks for a one-shot call of n inputs of
- * `count` elements whose output is 16-B aligned, on a GPU of `cus` CUs (no
+ * `count` elements whose output is 16-B aligned and whose store form is left
+ * to size (store_policy 0), on a GPU of `cus` CUs (no
  * device is queried: host code and tests can ask; a plan asks with the sum
  * of its computes' elements and their packet-weighted mean n).  A launch on
  * a capturing stream or hipStreamPerThread takes the static schedule. */
