@@ -192,8 +192,43 @@ def c4(stream):
             torch.cuda.empty_cache()
 
 
+def c4_engines(stream):
+    """Config 4's batched f32 plans (8 inputs in 1 MiB computes) at 16 / 64 /
+    256 MiB per input with the default store form: AUTO against each engine,
+    interleaved rounds, same bits."""
+    variants = {"auto": None, "tile": dict(engine=1), "tile_dyn": dict(engine=1, schedule=2), "phase": dict(engine=2)}
+    for mib in (16, 64, 256):
+        c = (mib << 20) // 4
+        ins = [torch.empty(c, device="cuda") for _ in range(8)]
+        for k, t in enumerate(ins):
+            hiccl_amd.fill_uniform(t, B.SEED, k)
+        outs = {v: torch.empty(c, device="cuda") for v in variants}
+        plans = {}
+        step = (1 << 20) // 4
+        for v, cfg in variants.items():
+            comp = hiccl_amd.Compute(torch.float32, device=torch.cuda.current_device(), config=cfg)
+            for off in range(0, c, step):
+                comp.add([(x, off) for x in ins], (outs[v], off), min(step, c - off), compid=0)
+            plans[v] = comp
+        t = timed({v: (lambda p=p: p.start(stream=stream)) for v, p in plans.items()})
+        torch.cuda.synchronize()
+        ok = all(torch.equal(outs["auto"].view(torch.int32), o.view(torch.int32)) for o in outs.values())
+        r = {"mode": "store_threshold", "kind": "c4_engines", "mib_per_input": mib, "bits_ok": bool(ok),
+             "auto_engine": plans["auto"].engine(), "store_policy": plans["auto"].store_policy()}
+        for k, v in t.items():
+            r[f"{k}_GBps"] = round(9 * c * 4 / (v * 1e-3) / 1e9, 1)
+        print(json.dumps(r), flush=True)
+        for p in plans.values():
+            p.close()
+        del ins, outs
+        torch.cuda.empty_cache()
+
+
 def main():
     stream = torch.cuda.current_stream()
+    if len(sys.argv) > 1 and sys.argv[1] == "c4eng":
+        c4_engines(stream)
+        return 0
     if len(sys.argv) > 1 and sys.argv[1] == "c4":
         c4(stream)
         return 0
