@@ -143,7 +143,8 @@ def engines(stream):
     c = (256 << 20) // 4
     variants = {"auto": None, "tile": dict(engine=1), "tile_dyn": dict(engine=1, schedule=2),
                 "phase": dict(engine=2)}
-    for n in (2, 3, 4, 8):
+    ns = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else (2, 3, 4, 8)
+    for n in ns:
         ins = [torch.empty(c, device="cuda") for _ in range(n)]
         for k, t in enumerate(ins):
             hiccl_amd.fill_uniform(t, B.SEED, k)
