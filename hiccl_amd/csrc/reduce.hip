@@ -1268,7 +1268,15 @@ int auto_engine(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
   const int acc = c.acc;
   if (auto_wide_unroll(npkt, n, dtype, c, dev)) return HICCL_ENGINE_TILE;
   const bool packed_ok = !(dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_WIDE);
-  if (n >= kDynMinInputs && packed_ok) {
+  // Round 5: a launch that stores write-through (store form left to size, at
+  // most wt_cap written; f32) runs faster on the phased engine wherever the
+  // dynamic tiles would otherwise take it -- 256 MiB per input, n = 8 / 16 /
+  // 32 / 64: 6.49 / 6.45 / 6.71 / 6.59 vs 6.37-6.40 TB/s interleaved
+  // (profiles/r05ab_c3_engines_many.jsonl; n = 8 on another box 6.50 vs
+  // 6.42, r05v_c3_engines.jsonl), config 4's 256 MiB plan 6.60 vs 6.44
+  // (r05aa_c4_engines.jsonl); at 1 GiB (nt) the tiles keep their lead.
+  const bool wt_f32 = c.store_auto && dtype == HICCL_FLOAT32 && npkt * kPacket <= wt_cap(n);
+  if (n >= kDynMinInputs && packed_ok && !wt_f32) {
     const uint64_t tickets = npkt / ((uint64_t)kDefBlock * kDefUnroll) / default_grab(HICCL_ENGINE_TILE, n);
     if (tickets >= kTileMinTicketsPerWG * (uint64_t)device_cus(dev)) return HICCL_ENGINE_TILE;
   }
@@ -1296,8 +1304,7 @@ int auto_engine(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
   // the phased engine at three inputs: 6.80 vs 6.62 TB/s interleaved at
   // 3 x 256 MiB (profiles/r05v_c3_engines.jsonl; 6.86 vs 6.63 on another
   // box, r05r_nway.jsonl); at two and four inputs the nt table holds.
-  if (n >= 2.5 && n < 3.5 && c.store_auto && dtype == HICCL_FLOAT32 && npkt * kPacket <= wt_cap(n))
-    return HICCL_ENGINE_TILE;
+  if (n >= 2.5 && n < 3.5 && wt_f32) return HICCL_ENGINE_TILE;
   if (n < kDynMinInputs) return per_cu >= 4 && round_eff >= 0.89 ? HICCL_ENGINE_PHASE : HICCL_ENGINE_TILE;
   // many inputs, under the dynamic tiles' ticket count: PHASE from one
   // whole chunk per CU unless too much of the last round idles (f32 n = 8 at
