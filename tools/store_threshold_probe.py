@@ -198,26 +198,29 @@ def c4_engines(stream):
     256 MiB per input with the default store form: AUTO against each engine,
     interleaved rounds, same bits."""
     variants = {"auto": None, "tile": dict(engine=1), "tile_dyn": dict(engine=1, schedule=2), "phase": dict(engine=2)}
+    dtype = torch.bfloat16 if len(sys.argv) > 2 and sys.argv[2] == "bf16" else torch.float32
+    esz = torch.tensor([], dtype=dtype).element_size()
+    bits = torch.int16 if dtype == torch.bfloat16 else torch.int32
     for mib in (16, 64, 256):
-        c = (mib << 20) // 4
-        ins = [torch.empty(c, device="cuda") for _ in range(8)]
+        c = (mib << 20) // esz
+        ins = [torch.empty(c, dtype=dtype, device="cuda") for _ in range(8)]
         for k, t in enumerate(ins):
             hiccl_amd.fill_uniform(t, B.SEED, k)
-        outs = {v: torch.empty(c, device="cuda") for v in variants}
+        outs = {v: torch.empty(c, dtype=dtype, device="cuda") for v in variants}
         plans = {}
-        step = (1 << 20) // 4
+        step = (1 << 20) // esz
         for v, cfg in variants.items():
-            comp = hiccl_amd.Compute(torch.float32, device=torch.cuda.current_device(), config=cfg)
+            comp = hiccl_amd.Compute(dtype, device=torch.cuda.current_device(), config=cfg)
             for off in range(0, c, step):
                 comp.add([(x, off) for x in ins], (outs[v], off), min(step, c - off), compid=0)
             plans[v] = comp
         t = timed({v: (lambda p=p: p.start(stream=stream)) for v, p in plans.items()})
         torch.cuda.synchronize()
-        ok = all(torch.equal(outs["auto"].view(torch.int32), o.view(torch.int32)) for o in outs.values())
-        r = {"mode": "store_threshold", "kind": "c4_engines", "mib_per_input": mib, "bits_ok": bool(ok),
-             "auto_engine": plans["auto"].engine(), "store_policy": plans["auto"].store_policy()}
+        ok = all(torch.equal(outs["auto"].view(bits), o.view(bits)) for o in outs.values())
+        r = {"mode": "store_threshold", "kind": "c4_engines", "dtype": str(dtype).split(".")[-1], "mib_per_input": mib,
+             "bits_ok": bool(ok), "auto_engine": plans["auto"].engine(), "store_policy": plans["auto"].store_policy()}
         for k, v in t.items():
-            r[f"{k}_GBps"] = round(9 * c * 4 / (v * 1e-3) / 1e9, 1)
+            r[f"{k}_GBps"] = round(9 * c * esz / (v * 1e-3) / 1e9, 1)
         print(json.dumps(r), flush=True)
         for p in plans.values():
             p.close()
