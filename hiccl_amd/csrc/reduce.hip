@@ -1269,14 +1269,17 @@ int auto_engine(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
   if (auto_wide_unroll(npkt, n, dtype, c, dev)) return HICCL_ENGINE_TILE;
   const bool packed_ok = !(dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_WIDE);
   // Round 5: a launch that stores write-through (store form left to size, at
-  // most wt_cap written; f32) runs faster on the phased engine wherever the
+  // most wt_cap written; f32, bf16) runs faster on the phased engine wherever the
   // dynamic tiles would otherwise take it -- 256 MiB per input, n = 8 / 16 /
   // 32 / 64: 6.49 / 6.45 / 6.71 / 6.59 vs 6.37-6.40 TB/s interleaved
   // (profiles/r05ab_c3_engines_many.jsonl; n = 8 on another box 6.50 vs
   // 6.42, r05v_c3_engines.jsonl), config 4's 256 MiB plan 6.60 vs 6.44
-  // (r05aa_c4_engines.jsonl); at 1 GiB (nt) the tiles keep their lead.
-  const bool wt_f32 = c.store_auto && dtype == HICCL_FLOAT32 && npkt * kPacket <= wt_cap(n);
-  if (n >= kDynMinInputs && packed_ok && !wt_f32) {
+  // (r05aa_c4_engines.jsonl; bf16 6.62 vs 6.33, r05ad_c4_engines_bf16.jsonl);
+  // at 1 GiB (nt) the tiles keep their lead.
+  const bool wt = c.store_auto && npkt * kPacket <= wt_cap(n);
+  const bool wt_f32 = wt && dtype == HICCL_FLOAT32;
+  const bool wt_many = wt && (dtype == HICCL_FLOAT32 || (dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_NATIVE));
+  if (n >= kDynMinInputs && packed_ok && !wt_many) {
     const uint64_t tickets = npkt / ((uint64_t)kDefBlock * kDefUnroll) / default_grab(HICCL_ENGINE_TILE, n);
     if (tickets >= kTileMinTicketsPerWG * (uint64_t)device_cus(dev)) return HICCL_ENGINE_TILE;
   }

@@ -159,6 +159,8 @@ def test_auto_choice_rule_table_on_host():
         ((f32, 1 << 26, 8), (P, 16, 1, 0)),      # C3, many inputs, write-through (round 5): PHASE
         ((f32, 1 << 26, 64), (P, 16, 1, 0)),
         ((f32, 1 << 27, 8), (T, 4, 1, 1)),       # 512 MiB written (nt): 128 tickets per workgroup, tiles
+        ((bf16, 1 << 27, 8), (P, 16, 1, 0)),     # bf16 256 MiB per input, write-through: PHASE too
+        ((bf16, 1 << 28, 8), (T, 4, 1, 1)),      # bf16 512 MiB (nt): tiles
         ((f32, 1 << 28, 2), (T, 16, 1, 1)),      # 1 GiB per input, few inputs: wide tiles
         ((f32, 1 << 28, 3), (T, 8, 1, 1)),
         ((f32, 40 * MiB // 4, 3), (T, 4, 1, 0)),  # 1.25 chunks per CU: tiles
