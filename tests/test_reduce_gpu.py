@@ -490,16 +490,18 @@ def test_wide_tile_size_with_caller_shape_runs(oracle, config):
 
 def test_plan_auto_engine_bf16():
     """bf16 with >= 5 inputs: AUTO takes TILE only from 64 tickets per
-    workgroup (n = 8: 2^27 elements per input on 256 CUs), PHASE below;
-    either engine gives the other's bits, and the TILE result matches an
-    in-order bf16 sum on the host (sampled)."""
+    workgroup (n = 8: 2^27 elements per input on 256 CUs) and above the
+    write-through cap (round 5: at 2^27 a launch writes 256 MiB and stores
+    write-through, where PHASE leads), PHASE below; either engine gives the
+    other's bits, and the result matches an in-order bf16 sum on the host
+    (sampled)."""
     P, T = hiccl_amd.HICCL_ENGINE_PHASE, hiccl_amd.HICCL_ENGINE_TILE
-    big = 1 << 27
+    big = 1 << 28
     base = torch.empty(big + 64, dtype=torch.bfloat16, device=DEV)
     hiccl_amd.fill_uniform(base, 91, 0)
     offs = (0, 0, 1, 3, 0, 2, 7, 5)
     full = 256 == torch.cuda.get_device_properties(0).multi_processor_count
-    for cnt, expect, other in ((big, T, P), (big // 2, P, T)):
+    for cnt, expect, other in ((big, T, P), (big // 2, P, T), (big // 4, P, T)):
         ins = [(base, o) for o in offs]
         outs = []
         for eng in (hiccl_amd.HICCL_ENGINE_AUTO, other):
