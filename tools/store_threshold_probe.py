@@ -228,8 +228,45 @@ def c4_engines(stream):
         torch.cuda.empty_cache()
 
 
+def c2_loads(stream):
+    """Config 2's bucket (8 x 1 GiB) as a one-compute plan with the default
+    loads (nt) and with system-scope loads (the peer-load form, sc0 sc1:
+    another path through the caches), each with nt and write-through
+    stores, against the one-shot launch; interleaved rounds, same bits."""
+    n, c = 8, 1 << 28
+    ins = [torch.empty(c, device="cuda") for _ in range(n)]
+    for k, t in enumerate(ins):
+        hiccl_amd.fill_uniform(t, B.SEED, k)
+    outs, plans = {}, {}
+    for name, peer, cfg in (("plan_nt", 0, dict(store_policy=2)), ("plan_sysload", 2, dict(store_policy=2)),
+                            ("plan_sysload_wt", 2, dict(store_policy=4)), ("plan_wt", 0, dict(store_policy=4))):
+        outs[name] = torch.empty(c, device="cuda")
+        comp = hiccl_amd.Compute(torch.float32, device=torch.cuda.current_device(), config=dict(cfg, engine=1, unroll=4))
+        if peer:
+            comp.set_peer(peer)
+        comp.add(ins, outs[name], c, compid=0)
+        plans[name] = comp
+    outs["oneshot"] = torch.empty(c, device="cuda")
+    fns = {k: (lambda p=p: p.start(stream=stream)) for k, p in plans.items()}
+    fns["oneshot"] = lambda: hiccl_amd.reduce(outs["oneshot"], ins, stream=stream)
+    t = timed(fns, steps=10, warmup=2, rounds=5)
+    torch.cuda.synchronize()
+    ok = all(torch.equal(outs["oneshot"].view(torch.int32), o.view(torch.int32)) for o in outs.values())
+    nb = (n + 1) * c * 4
+    r = {"mode": "store_threshold", "kind": "c2_loads", "bits_ok": bool(ok)}
+    for k, v in t.items():
+        r[f"{k}_ms"] = round(v, 4)
+        r[f"{k}_frac"] = round(nb / (v * 1e-3) / 1e9 / 8000.0, 4)
+    print(json.dumps(r), flush=True)
+    for p in plans.values():
+        p.close()
+
+
 def main():
     stream = torch.cuda.current_stream()
+    if len(sys.argv) > 1 and sys.argv[1] == "c2loads":
+        c2_loads(stream)
+        return 0
     if len(sys.argv) > 1 and sys.argv[1] == "c4eng":
         c4_engines(stream)
         return 0
