@@ -82,6 +82,8 @@ _SIGS = {
                                        ctypes.POINTER(ReduceConfig)]),
     "hiccl_reduce_auto_choice": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_double,
                                                 ctypes.c_int, _vp, _vp, _vp, _vp]),
+    "hiccl_reduce_auto_choice_ex": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ReduceConfig), ctypes.c_size_t,
+                                                   ctypes.c_double, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     "hiccl_reduce_plan_create": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int]),
     "hiccl_reduce_plan_set_acc": (ctypes.c_int, [_vp, ctypes.c_int]),
     "hiccl_reduce_plan_set_engine": (ctypes.c_int, [_vp, ctypes.c_int]),

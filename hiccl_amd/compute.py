@@ -96,6 +96,21 @@ def reduce_ptrs(dtype_code, out_ptr, in_ptrs, count, stream=None, config=None):
     L.check(rc, "hiccl_reduce")
 
 
+def auto_choice(dtype, count, n, config=None, cus=256):
+    """What a one-shot call (and a one-compute plan at TILE unroll 2 / 4 or
+    AUTO) resolves to on a GPU of ``cus`` CUs, without a device:
+    ``hiccl_reduce_auto_choice_ex``.  ``dtype``: a torch dtype or an
+    HICCL_* code; ``n`` may be a plan's packet-weighted mean.  Returns a dict
+    with engine, unroll, blocks_per_cu, dynamic and store_policy (2 nt, 4
+    write-through); raises HicclError for a config no kernel has."""
+    dt = L.DTYPE_OF_TORCH[dtype] if isinstance(dtype, torch.dtype) else int(dtype)
+    cfg = ctypes.byref(L.ReduceConfig(**config)) if config else None
+    out = [ctypes.c_int() for _ in range(5)]
+    rc = L.lib().hiccl_reduce_auto_choice_ex(dt, cfg, count, float(n), cus, *[ctypes.byref(v) for v in out])
+    L.check(rc, "hiccl_reduce_auto_choice_ex")
+    return dict(zip(("engine", "unroll", "blocks_per_cu", "dynamic", "store_policy"), (v.value for v in out)))
+
+
 class Compute:
     """``HiCCL::Compute<T>`` (source/compute.h:26-204) on the batched plan.
 

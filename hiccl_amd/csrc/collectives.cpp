@@ -130,9 +130,12 @@ static int bench_json(const char *path, HiCCL::Comm<Type> &coll, Type *sendbuf_d
   // stream-ordered enqueue and final sync), microseconds per step, MAX over
   // ranks of each part
   // (HICCL_HOST_SPLIT_RUNS extra runs, default 1, 0: none -- never numiter
-  // more full collectives inside a bench leg's time budget)
+  // more full collectives inside a bench leg's time budget).  Rank 0's value
+  // for every rank: each run is a barrier plus a full collective, so ranks
+  // reading different values (a per-rank environment) would deadlock.
   int split_runs = 1;
   if (const char *e = std::getenv("HICCL_HOST_SPLIT_RUNS")) split_runs = std::max(0, std::atoi(e));
+  MPI_Bcast(&split_runs, 1, MPI_INT, 0, CommBench::comm_mpi);
   coll.set_step_timing(true);
   for (int r = 0; r < split_runs; r++) {
     MPI_Barrier(CommBench::comm_mpi);

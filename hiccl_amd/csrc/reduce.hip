@@ -955,15 +955,21 @@ __global__ __launch_bounds__(kProgBlock) void k_program(ProgArgs a) {
     } else if (tid == 0) {
       prog_gate_wait(a, seq);
       // Fenced mode: an agent-scope acquire closes the relaxed gate polls,
-      // pairing with workgroup 0's agent-scope release store of the gate.
-      // Workgroup 0 acquired the peers' tokens at system scope before that
-      // release, so by transitivity every peer write a token covers happens
-      // before this workgroup's units (the memory model's guarantee, not
-      // the kernel-boundary cache argument `light` rests on).  Agent scope,
-      // not system: both ends of this hand-off run on this GPU; a
-      // system-scope acquire per workgroup (1,024 L2 invalidations per
-      // launch) cost ~8 us per C5 step (profiles/r04f_progstep.jsonl).
-      // The workgroup barrier below carries it to the other lanes.
+      // pairing with workgroup 0's agent-scope release store of the gate,
+      // which follows workgroup 0's system-scope acquire of the peers'
+      // tokens.  That orders this workgroup after the tokens for writes made
+      // on THIS GPU.  It is not a guarantee for a peer GPU's writes: on a
+      // part with several XCDs workgroup 0's system-scope acquire
+      // invalidates only its own XCD's L2, and an agent-scope acquire on
+      // another XCD does not drop non-coherent L2 lines there.  Peer data
+      // stays visible because no L2 holds a line of it (peer puts store
+      // write-through, HICCL_PEER_STORES; fused reads load system-scope,
+      // HICCL_PEER_LOADS; and the kernel-start invalidate) -- the same
+      // cache argument `light` rests on, and unconfirmed until a run with
+      // one GPU per rank.  Agent scope, not system: a system-scope acquire
+      // per workgroup (1,024 L2 invalidations per launch) cost ~8 us per
+      // C5 step (profiles/r04f_progstep.jsonl).  The workgroup barrier
+      // below carries it to the other lanes.
       if (!a.light) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
@@ -1218,11 +1224,14 @@ int phase_p_dtype(int dtype, int acc) {
 struct Cfg {
   int block, unroll, bpc, nt, acc, grid, store, engine, schedule, grab, drain;
   bool store_auto;  // store_policy 0: the store form follows the launch's size (wt_cap)
+  bool wt;          // the launch stores write-through by size: decided BEFORE the engine
+                    // (oneshot_cfg, plan_cfg), since AUTO's engine rules differ under it
 };
 
 // Raw config: zero block/unroll stay zero until the engine is known.
 Cfg resolve(const hiccl_reduce_config_t *c) {
-  Cfg r{0, 0, 0, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO, HICCL_SCHED_AUTO, 0, 0, true};
+  Cfg r{0, 0, 0, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO, HICCL_SCHED_AUTO, 0, 0, true,
+        false};
   if (c) {
     r.block = c->block;
     r.unroll = c->unroll;
@@ -1275,8 +1284,9 @@ int auto_engine(uint64_t npkt, double n, int dtype, const Cfg &c, int dev) {
   // (profiles/r05ab_c3_engines_many.jsonl; n = 8 on another box 6.50 vs
   // 6.42, r05v_c3_engines.jsonl), config 4's 256 MiB plan 6.60 vs 6.44
   // (r05aa_c4_engines.jsonl; bf16 6.62 vs 6.33, r05ad_c4_engines_bf16.jsonl);
-  // at 1 GiB (nt) the tiles keep their lead.
-  const bool wt = c.store_auto && npkt * kPacket <= wt_cap(n);
+  // at 1 GiB (nt) the tiles keep their lead.  `c.wt` is the store form the
+  // launch actually takes (by size, where a write-through kernel exists).
+  const bool wt = c.wt;
   const bool wt_f32 = wt && dtype == HICCL_FLOAT32;
   const bool wt_many = wt && (dtype == HICCL_FLOAT32 || (dtype == HICCL_BFLOAT16 && acc == HICCL_ACC_NATIVE));
   if (n >= kDynMinInputs && packed_ok && !wt_many) {
@@ -1549,9 +1559,53 @@ std::string plan_shape_error(const Cfg &c, int dtype) {
     return "";
   }
   if (c.block != kPlanBlock) return "plan kernels run the TILE engine at block 256 only";
+  if (c.store == kPolStoreSys) {
+    if (!pick_plan(dtype, c.acc, HICCL_ENGINE_TILE, c.unroll, plan_pol(HICCL_PEER_STORES)))
+      return "write-through plan kernels (store_policy 4) run the TILE engine at unroll 4 (f32 / bf16: 2 or 4) only";
+    return "";
+  }
   if (!pick_plan(dtype, c.acc, HICCL_ENGINE_TILE, c.unroll))
     return "plan kernels run the TILE engine at unroll 4 (f32 / bf16: 1, 2, 4, 8 or 16) only";
   return "";
+}
+
+// The one-shot call's configuration, engine and store form resolved.  The
+// store form is decided first: write-through (system scope) by size -- at
+// most wt_cap written -- when the config leaves it open, loads are nt (the
+// only write-through kernels) and an explicit TILE unroll is 2 or 4 (the
+// plan's rule, plan_store_peer: one rule for both), since AUTO's engine rules
+// differ under it (auto_engine).  If the shape finish_cfg then picks lacks a
+// write-through kernel, the call keeps nt stores and its engine is chosen
+// again for them.  n > 64 inputs run on the plan kernel (reduce_via_table),
+// whose kernels decide.  hiccl_reduce_ex and hiccl_reduce_auto_choice_ex
+// share it.
+Cfg oneshot_cfg(int dtype, const hiccl_reduce_config_t *cfg, uint64_t npkt, uint64_t out_bytes, double n,
+                int dev) {
+  const Cfg raw = resolve(cfg);
+  Cfg c = raw;
+  const bool u_ok = !raw.unroll || raw.unroll == 2 || raw.unroll == kDefUnroll || raw.engine == HICCL_ENGINE_PHASE;
+  c.wt = raw.store_auto && raw.nt == kDefPol % 10 && u_ok && out_bytes <= wt_cap(dtype == HICCL_BYTES ? 1.0 : n);
+  finish_cfg(c, npkt, n, dtype, dev);
+  if (!c.wt) return c;
+  Cfg w = c;
+  w.store = kPolStoreSys;
+  if (n > kMaxArgInputs ? pick_plan(dtype, w.acc, w.engine, w.unroll, plan_pol(HICCL_PEER_STORES)) != nullptr
+                        : pick_single_dtype(dtype, w) != nullptr)
+    return w;
+  c = raw;
+  finish_cfg(c, npkt, n, dtype, dev);
+  return c;
+}
+
+// The enumerated fields of a one-shot config (before finish_cfg).
+int check_cfg_fields(const Cfg &c, const std::string &who) {
+  if (c.acc != HICCL_ACC_NATIVE && c.acc != HICCL_ACC_WIDE) return fail(hipErrorInvalidValue, who + ": bad acc mode");
+  if (c.engine < HICCL_ENGINE_AUTO || c.engine > HICCL_ENGINE_PHASE)
+    return fail(hipErrorInvalidValue, who + ": bad engine");
+  if (c.schedule < HICCL_SCHED_AUTO || c.schedule > HICCL_SCHED_DYNAMIC)
+    return fail(hipErrorInvalidValue, who + ": bad schedule");
+  if (c.grab < 0 || c.grab > 4096) return fail(hipErrorInvalidValue, who + ": bad grab");
+  return 0;
 }
 
 uint64_t tiles_for(uint64_t npkt, uint64_t tile) {
@@ -1586,28 +1640,13 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
   if (count == 0) return 0;
   if (dtype == HICCL_BYTES && n != 1) return fail(hipErrorInvalidValue, "hiccl_reduce: HICCL_BYTES copies need n == 1");
   if (int e = check_buffers(out, in, n, count, esz)) return e;
-  Cfg c = resolve(cfg);
-  if (c.acc != HICCL_ACC_NATIVE && c.acc != HICCL_ACC_WIDE)
-    return fail(hipErrorInvalidValue, "hiccl_reduce: bad acc mode");
-  if (c.engine < HICCL_ENGINE_AUTO || c.engine > HICCL_ENGINE_PHASE)
-    return fail(hipErrorInvalidValue, "hiccl_reduce: bad engine");
-  if (c.schedule < HICCL_SCHED_AUTO || c.schedule > HICCL_SCHED_DYNAMIC)
-    return fail(hipErrorInvalidValue, "hiccl_reduce: bad schedule");
-  if (c.grab < 0 || c.grab > 4096) return fail(hipErrorInvalidValue, "hiccl_reduce: bad grab");
+  if (int e = check_cfg_fields(resolve(cfg), "hiccl_reduce")) return e;
   hipStream_t s = (hipStream_t)stream;
   const int dev = current_device();
   Split sp = split_on(out, count, esz);
-  finish_cfg(c, sp.npkt, n, dtype, dev);
-  // the store form by size, as a plan's (plan_store_peer): write-through when
-  // the call writes at most wt_cap(n) bytes, its config leaves the store form
-  // open and its shape has a write-through kernel
-  if ((!cfg || cfg->store_policy == 0) && (uint64_t)count * esz <= wt_cap(dtype == HICCL_BYTES ? 1.0 : n)) {
-    Cfg w = c;
-    w.store = kPolStoreSys;
-    if (n > kMaxArgInputs ? pick_plan(dtype, w.acc, w.engine, w.unroll, plan_pol(HICCL_PEER_STORES)) != nullptr
-                          : pick_single_dtype(dtype, w) != nullptr)
-      c = w;
-  }
+  // engine, shape and store form (write-through by size, as a plan's:
+  // plan_store_peer)
+  Cfg c = oneshot_cfg(dtype, cfg, sp.npkt, (uint64_t)count * esz, n, dev);
   if (c.bpc < 1 || c.bpc > 64) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: blocks_per_cu");
   if (c.grid < 0) return fail(hipErrorInvalidValue, "hiccl_reduce_ex: grid < 0");
   if (n > kMaxArgInputs) {
@@ -1663,30 +1702,38 @@ int hiccl_reduce_bf16(uint16_t *out, const uint16_t *const *in, int n, size_t co
   return hiccl_reduce_ex(HICCL_BFLOAT16, out, (const void *const *)in, n, count, stream, nullptr);
 }
 
-int hiccl_reduce_auto_choice(int dtype, int acc, size_t count, double n, int cus, int *engine, int *unroll,
-                             int *blocks_per_cu, int *dynamic) {
+int hiccl_reduce_auto_choice_ex(int dtype, const hiccl_reduce_config_t *cfg, size_t count, double n, int cus,
+                                int *engine, int *unroll, int *blocks_per_cu, int *dynamic, int *store_policy) {
   const size_t esz = esize(dtype);
   if (!esz) return fail(hipErrorInvalidValue, "auto_choice: unknown dtype");
-  if (acc != HICCL_ACC_NATIVE && acc != HICCL_ACC_WIDE) return fail(hipErrorInvalidValue, "auto_choice: bad acc");
   if (cus <= 0 || n < 0) return fail(hipErrorInvalidValue, "auto_choice: cus must be > 0 and n >= 0");
+  if (int e = check_cfg_fields(resolve(cfg), "auto_choice")) return e;
   struct CusOverride {  // no device query: the choice for `cus` CUs (reset on every exit)
     explicit CusOverride(int c) { t_cus_override = c; }
     ~CusOverride() { t_cus_override = 0; }
   } scoped(cus);
-  hiccl_reduce_config_t z;
-  memset(&z, 0, sizeof(z));
-  z.acc = acc;
-  Cfg c = resolve(&z);
   const uint64_t npkt = (uint64_t)count * esz / kPacket;
-  finish_cfg(c, npkt, n, dtype, -1);
+  const Cfg c = oneshot_cfg(dtype, cfg, npkt, (uint64_t)count * esz, n, -1);
+  // the same refusals as hiccl_reduce_ex: a shape no kernel has is an error
+  const bool has = n > kMaxArgInputs ? plan_shape_error(c, dtype).empty() : pick_single_dtype(dtype, c) != nullptr;
+  if (!has) return fail(hipErrorInvalidValue, "auto_choice: no kernel for this config and dtype");
   const uint64_t units = tiles_for(npkt, (uint64_t)c.block * c.unroll);  // tiles or phased chunks
-  const uint64_t grid = std::min<uint64_t>((uint64_t)cus * c.bpc, units);
-  const bool dyn = wants_dynamic(c.engine, n, units, grid, c.schedule, 0, c.unroll);
+  const uint64_t grid = std::min<uint64_t>(c.grid > 0 ? (uint64_t)c.grid : (uint64_t)cus * c.bpc, units);
+  const bool dyn = wants_dynamic(c.engine, n, units, grid, c.schedule, (uint32_t)c.grab, c.unroll);
   if (engine) *engine = c.engine;
   if (unroll) *unroll = c.unroll;
   if (blocks_per_cu) *blocks_per_cu = c.bpc;
   if (dynamic) *dynamic = dyn ? 1 : 0;
+  if (store_policy) *store_policy = c.store + 1;
   return 0;
+}
+
+int hiccl_reduce_auto_choice(int dtype, int acc, size_t count, double n, int cus, int *engine, int *unroll,
+                             int *blocks_per_cu, int *dynamic) {
+  hiccl_reduce_config_t z;
+  memset(&z, 0, sizeof(z));
+  z.acc = acc;
+  return hiccl_reduce_auto_choice_ex(dtype, &z, count, n, cus, engine, unroll, blocks_per_cu, dynamic, nullptr);
 }
 
 // ---------------------------------------------------------------- plan ----
@@ -1779,6 +1826,9 @@ int plan_eff_peer(const hiccl_reduce_plan *p) { return p->peer | plan_store_peer
 Cfg plan_cfg(const hiccl_reduce_plan *p, uint64_t npkt, double mean_n) {
   Cfg c = resolve(&p->req);
   const bool auto_unroll = !c.unroll;
+  // AUTO's engine rules follow the store form the launches take by size
+  // (plan_store_peer already checked the shape has a write-through kernel)
+  c.wt = c.store_auto && (plan_store_peer(p) & HICCL_PEER_STORES);
   finish_cfg(c, npkt, mean_n, p->dtype, p->device);  // (kPlanBlock == kDefBlock)
   // peer and write-through policies exist at TILE U = 4 / 2 only: wide tiles
   // become U = 4
@@ -1915,8 +1965,10 @@ int reduce_via_table(int dtype, const Cfg &c, void *out, const void *const *in, 
   // hipMemcpyAsync from pageable memory returns once the source is consumed,
   // so `host` may go out of scope (never under capture: refused by the caller)
   if (int e = check_hip(hipMemcpyAsync(dmem, host.data(), L.bytes, hipMemcpyHostToDevice, s),
-                        "hiccl_reduce: table upload"))
+                        "hiccl_reduce: table upload")) {
+    (void)hipFreeAsync(dmem, s);
     return e;
+  }
   PlanArgs a;
   memset(&a, 0, sizeof(a));
   a.desc = (const PlanDesc *)(dmem + L.desc);
@@ -1925,9 +1977,13 @@ int reduce_via_table(int dtype, const Cfg &c, void *out, const void *const *in, 
   a.stride = (uint32_t)n;
   a.t_begin = 0;
   a.t_end = tiles_for(sp.npkt, unit_pkts(c.engine, dtype, c.acc, c.unroll));
-  // (one-shot: nt stores unless the caller asked for write-through, store_policy 4)
+  // the store form oneshot_cfg decided: write-through by size or on request
+  // (store_policy 4), else nt
   const int pol = c.store == kPolStoreSys ? plan_pol(HICCL_PEER_STORES) : kDefPol;
-  if (int e = launch_plan(a, dtype, c, n, current_device(), s, pol)) return e;
+  if (int e = launch_plan(a, dtype, c, n, current_device(), s, pol)) {
+    (void)hipFreeAsync(dmem, s);  // nothing launched reads it
+    return e;
+  }
   return check_hip(hipFreeAsync(dmem, s), "hiccl_reduce: hipFreeAsync");
 }
 

@@ -138,9 +138,14 @@ typedef struct {
   int store_policy;  /* stores: 1 plain, 2 nt, 3 sc1 (write-through, line dropped from L2),
                         4 system-scope write-through (sc0 sc1).  0: 4 when the launch
                         writes at most 256 MiB of sums (two or more inputs) or 32 MiB
-                        of copies (one input) and its shape has a write-through
-                        kernel (TILE unroll 1 / 2 / 4, PHASE's default shape) -- no
-                        dirty L2 lines left for the kernel boundary -- else 2 */
+                        of copies (one input), its loads are nt and its shape has a
+                        write-through kernel -- no dirty L2 lines left for the kernel
+                        boundary -- else 2.  The shapes the size rule applies to,
+                        one-shot calls and plans alike: AUTO, TILE unroll 2 / 4,
+                        PHASE's default shape (an explicit TILE unroll 1, 8 or 16
+                        stays nt; one-shot unroll 1 stores write-through on
+                        request, 4).  The store form is decided before AUTO picks
+                        the engine (its rules differ under write-through) */
   int engine;        /* hiccl_engine_t */
   int schedule;      /* hiccl_schedule_t */
   int grab;          /* dynamic schedule: units per ticket (0 = default: PHASE 1,
@@ -160,6 +165,15 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
  * a capturing stream or hipStreamPerThread takes the static schedule. */
 int hiccl_reduce_auto_choice(int dtype, int acc, size_t count, double n, int cus, int *engine, int *unroll,
                              int *blocks_per_cu, int *dynamic);
+/* The same for a one-shot call with config `cfg` (NULL = defaults), the same
+ * resolution hiccl_reduce_ex makes -- store form first, then engine and
+ * shape -- plus the store form it takes (*store_policy: 2 nt, 4
+ * write-through; any pointer may be NULL).  A config no kernel has returns
+ * hipErrorInvalidValue, as hiccl_reduce_ex would.  A plan of one compute
+ * with TILE unroll 2 / 4 or AUTO resolves the same way (tests pin the GPU
+ * tier's AUTO expectations to this answer on the host). */
+int hiccl_reduce_auto_choice_ex(int dtype, const hiccl_reduce_config_t *cfg, size_t count, double n, int cus,
+                                int *engine, int *unroll, int *blocks_per_cu, int *dynamic, int *store_policy);
 
 /* ----------------------------------------------------------------------
  * Persistent plan: the C-ABI counterpart of the reference's Compute<T>
@@ -359,7 +373,11 @@ int hiccl_signal_wait_phases(const hiccl_signal_phase_t *phases, int nphases, co
  * add_plan appends the plan's computes as of this call (later adds to the
  *   plan are not seen); the plan's dtype must be the program's or
  *   HICCL_BYTES; native accumulation only.  Computes of several plans form
- *   one batch: they must not depend on each other.
+ *   one batch: they must not depend on each other.  Each plan's store form
+ *   carries over as the plan decided it (hiccl_reduce_plan_store_policy, by
+ *   that plan's own size): a program joining several plans may write more
+ *   than the 256 MiB / 32 MiB caps in one launch and still store
+ *   write-through (a pipeline step's batches are a few MiB).
  * launch: epochs[p] for every phase p (+ *epoch_dev when not NULL, read at
  *   run time: graph replays), err / timeout_s as hiccl_signal_wait.  The
  *   first launch (and the first after a change) uploads the program's tables

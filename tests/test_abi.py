@@ -147,34 +147,10 @@ def test_auto_choice_rule_table_on_host():
     """hiccl_reduce_auto_choice (no device queried): AUTO's engine / shape /
     schedule for the BASELINE configs and the round-3 mid-size rule
     (profiles/r03n_midsize.jsonl, r03q_sweep_manyn.jsonl)."""
+    from auto_table import RULE_CASES as cases
     T, P = L.HICCL_ENGINE_TILE, L.HICCL_ENGINE_PHASE
     f32, bf16 = L.HICCL_FLOAT32, L.HICCL_BFLOAT16
     MiB = 1 << 20
-    cases = [  # (dtype, elements per input, n) -> (engine, unroll, blocks per CU, dynamic)
-        ((f32, 1 << 28, 8), (T, 4, 1, 1)),       # C2: tiles on the ticket counter
-        ((f32, 1 << 26, 2), (T, 4, 1, 0)),       # C3, two inputs: static tiles
-        ((f32, 1 << 26, 3), (T, 4, 1, 0)),       # C3, 3 inputs, write-through (round 5): static tiles
-        ((f32, 1 << 26, 4), (P, 16, 1, 0)),      # C3, 4 inputs: 8 whole chunks per CU
-        ((f32, 1 << 27, 3), (P, 16, 1, 0)),      # 512 MiB written (nt): the phased engine
-        ((f32, 1 << 26, 8), (P, 16, 1, 0)),      # C3, many inputs, write-through (round 5): PHASE
-        ((f32, 1 << 26, 64), (P, 16, 1, 0)),
-        ((f32, 1 << 27, 8), (T, 4, 1, 1)),       # 512 MiB written (nt): 128 tickets per workgroup, tiles
-        ((bf16, 1 << 27, 8), (P, 16, 1, 0)),     # bf16 256 MiB per input, write-through: PHASE too
-        ((bf16, 1 << 28, 8), (T, 4, 1, 1)),      # bf16 512 MiB (nt): tiles
-        ((f32, 1 << 28, 2), (T, 16, 1, 1)),      # 1 GiB per input, few inputs: wide tiles
-        ((f32, 1 << 28, 3), (T, 8, 1, 1)),
-        ((f32, 40 * MiB // 4, 3), (T, 4, 1, 0)),  # 1.25 chunks per CU: tiles
-        ((f32, 32 * MiB // 4, 4), (T, 4, 1, 0)),  # one chunk per CU, 3-4 inputs: tiles
-        ((f32, 40 * MiB // 4, 8), (T, 4, 1, 0)),  # a last round 25 % busy: tiles
-        ((f32, 48 * MiB // 4, 8), (P, 16, 1, 0)),  # 75 % busy: PHASE
-        ((f32, 24 * MiB // 4, 16), (P, 16, 1, 0)),  # 16 inputs, 0.75 chunks per CU: PHASE
-        ((f32, 16 * MiB // 4, 16), (T, 4, 4, 0)),   # 0.5 per CU: tiles, 4 workgroups per CU
-        ((f32, 5 << 18, 2.4), (T, 2, 4, 0)),     # the C5 step's plan: half-size tiles
-        ((bf16, 40 * MiB // 2, 3), (T, 4, 1, 0)),  # bf16 native: the f32 rule
-        ((L.HICCL_FLOAT64, 40 * MiB // 8, 3), (T, 4, 1, 0)),  # f64 / u64 too (r03x_midsize_f64.jsonl)
-        ((L.HICCL_FLOAT64, (1 << 26) // 2, 3), (P, 16, 1, 0)),
-        ((L.HICCL_UINT64, 40 * MiB // 8, 8), (T, 4, 1, 0)),
-    ]
     for (dt, count, n), want in cases:
         assert _auto(dt, count, n) == want, (dt, count, n, _auto(dt, count, n), want)
     # 64 KiB phased chunks (bf16 with the f32 accumulator, int32): the same rule
@@ -190,6 +166,56 @@ def test_auto_choice_rule_table_on_host():
     import ctypes
     assert lib.hiccl_reduce_auto_choice(42, 0, 1024, 2.0, 256, None, None, None, None) == 1
     assert lib.hiccl_reduce_auto_choice(f32, 0, 1024, 2.0, 0, None, None, None, None) == 1
+
+
+def test_gpu_tier_auto_expectations_follow_the_rule():
+    """The GPU tier's AUTO expectations (tests/auto_table.py, read by
+    test_reduce_gpu.py) agree with the rule the library implements: every
+    engine row and every store-form row, answered on the host for 256 CUs.
+    A rule change not carried into the table fails HERE, in the CPU tier."""
+    import auto_table as A
+    for (dt, count, n, cfg), want in A.all_engine_rows():
+        got = hiccl_amd.auto_choice(dt, count, n, config=cfg)
+        assert got["engine"] == want, (dt, count, n, cfg, got, want)
+    for (dt, count, n, cfg), want in A.all_store_rows():
+        got = hiccl_amd.auto_choice(dt, count, n, config=cfg)
+        assert got["store_policy"] == want, (dt, count, n, cfg, got, want)
+    # the plain entry point is the _ex one with a default config
+    for (dt, count, n), want in A.RULE_CASES:
+        got = hiccl_amd.auto_choice(dt, count, n)
+        assert (got["engine"], got["unroll"], got["blocks_per_cu"], got["dynamic"]) == want
+
+
+def test_auto_choice_ex_store_form_and_refusals():
+    """hiccl_reduce_auto_choice_ex: the store form is decided before the
+    engine, on the shapes that have a write-through kernel (the
+    engine must not follow write-through measurements for a launch that
+    stays nt), and a config no kernel has is refused as hiccl_reduce_ex
+    refuses it."""
+    T, P = L.HICCL_ENGINE_TILE, L.HICCL_ENGINE_PHASE
+    f32 = L.HICCL_FLOAT32
+    c3 = (f32, 1 << 26, 3)  # 3 x 256 MiB: write-through by size -> static tiles
+    assert hiccl_amd.auto_choice(*c3) == dict(engine=T, unroll=4, blocks_per_cu=1, dynamic=0, store_policy=4)
+    # plain loads (nontemporal 1): no write-through kernel, so nt stores AND the nt engine table
+    got = hiccl_amd.auto_choice(*c3, config=dict(nontemporal=1))
+    assert (got["engine"], got["store_policy"]) == (P, 2), got
+    assert hiccl_amd.auto_choice(*c3, config=dict(store_policy=2))["engine"] == P
+    # explicit unroll 1 stays nt by size (one rule for one-shot calls and plans), write-through on request
+    assert hiccl_amd.auto_choice(*c3, config=dict(engine=T, unroll=1))["store_policy"] == 2
+    assert hiccl_amd.auto_choice(*c3, config=dict(engine=T, unroll=1, store_policy=4))["store_policy"] == 4
+    # above the cap: nt whatever the engine
+    assert hiccl_amd.auto_choice(f32, 1 << 28, 8)["store_policy"] == 2
+    # byte copies: 32 MiB cap
+    assert hiccl_amd.auto_choice(L.HICCL_BYTES, 32 << 20, 1)["store_policy"] == 4
+    assert hiccl_amd.auto_choice(L.HICCL_BYTES, (32 << 20) + 16, 1)["store_policy"] == 2
+    # refusals: write-through wide tiles (one-shot), and n > 64 on the plan kernel
+    for cfg, n in ((dict(store_policy=4, engine=T, unroll=8), 2), (dict(store_policy=4, engine=T, unroll=8), 65),
+                   (dict(store_policy=4, engine=T, unroll=1), 65), (dict(block=512, unroll=4), 70),
+                   (dict(engine=7), 2), (dict(acc=5), 2), (dict(schedule=9), 2)):
+        with pytest.raises(hiccl_amd.HicclError):
+            hiccl_amd.auto_choice(f32, 1 << 16, n, config=cfg)
+    # n > 64 with unroll 8 and nt: the plan kernel has it
+    assert hiccl_amd.auto_choice(f32, 1 << 16, 65, config=dict(engine=T, unroll=8))["unroll"] == 8
 
 
 def test_stream_ordered_defaults_resolve_as_stated(monkeypatch):

@@ -387,10 +387,13 @@ def test_driver_line_stays_compact():
             "data": "synthetic", "config": {"workload": "C2 ..."},
             "roofline": {"bound": "hbm", "achieved": 6530.0, "peak": 8000.0, "unit": "GB/s", "frac": 0.816,
                          "traffic": 9.66e9, "serial_rw_model": {"frac": 0.98, "frac_write_probe": 0.95},
-                         "traffic_from_profile": {"file": "profiles/r05b_pmc.json"}, "traffic_source": "x" * 200},
+                         "traffic_from_profile": {"file": "profiles/r05b_pmc.json", "box_kernel_ms": 1.4449,
+                                                  "fits_this_run": True, "over_algorithmic": 1.00024},
+                         "traffic_source": "x" * 200},
             "cpu_baseline": cpu, "parity_full": {"ok": True, "mismatches": 0, "words": 1 << 28, "against": "y" * 100},
             "device_props": {"gcn_arch": "gfx950", "cus": 256, "mem_clock_khz": 2000000},
-            "c2_misaligned": {"shifted_over_aligned": 1.007, "shifted_frac": 0.78,
+            "c2_misaligned": {"shifted_over_aligned": 1.007, "shifted_frac": 0.78, "shifted_over_headline": 1.09,
+                              "aligned_over_headline": 1.08,
                               "parity_sample_ok": {"aligned": True, "shifted": True}}, "c5": c5}
     out = bench.compact_line(line)
     text = json.dumps(out)
@@ -403,6 +406,9 @@ def test_driver_line_stays_compact():
     c = out["cpu_baseline"]
     assert (c["value"], c["cores"], c["kind"], c["spread_cause"]["slow_runs"]) == (400.0, 16, "reference", 3)
     assert "pass_ms" not in c and out["c2_misaligned"]["parity_ok"] is True
+    assert out["c2_misaligned"]["shifted_over_headline"] == 1.09 and out["c2_misaligned"]["aligned_over_headline"] == 1.08
+    assert r["traffic_profile"] == {"file": "profiles/r05b_pmc.json", "kernel_ms": 1.4449, "fits_this_run": True,
+                                    "x_alg": 1.00024}
     assert out["c5"]["stopped_after"] == "xccl" and out["c5"]["xccl"]["rc"] == 124
     assert out["c5"]["host"]["kat"] == "PASSED" and "host_split_us_per_step" not in out["c5"]["host"]
     assert out["c5"]["protocol_ab"]["baseline_ms"] == 31.5
@@ -417,3 +423,84 @@ def test_compact_c5_skipped_leg():
                             "env_scrubbed": {"HIP_VISIBLE_DEVICES": "0"}, "devices_counted_unmasked": 1})
     assert out == {"skipped": "2 ranks on 1 GPU(s): config 5 needs one GPU per rank"}
     assert bench.compact_c5({"skipped": "error: boom"}) == {"skipped": "error: boom"}
+
+
+C5_MODES = ("host", "stream_graph", "stream_graph_fused_noprog", "stream_graph_fused_fenced",
+            "flat_stream_graph_fused", "xccl", "stream_graph_fused")
+DRIVER_TAIL_CHARS = 3500  # the compact line's budget: BENCH_r04's whole stdout tail was 3,166 chars
+
+
+@pytest.mark.parametrize("failing", [0, 3, 7])
+def test_driver_line_keeps_every_c5_mode_at_n8(failing):
+    """At N = 8 the driver's one line must let a reader tell, per config-5
+    mode, whether the cross-GPU run passed, from SCALE_rNN.json alone: every
+    mode's kat, mode_used and rc, the leg's stopped_after and protocol_ab --
+    also when modes fail with long errors, all within the stdout tail
+    (VERDICT r05 item 6; reference config collectives/main.cpp:151-155)."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    c5 = {"workload": "C5: 8 ranks {1,4,2} {MPI,IPC,IPC} 2^25 floats per rank per chunk, pipedepth 128 " + "w" * 100,
+          "env_scrubbed": {"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}, "devices_counted_unmasked": 8}
+    for i, m in enumerate(C5_MODES):
+        bad = i >= len(C5_MODES) - failing
+        r = {"kat": "FAILED" if bad else "PASSED", "rc": 1 if bad else 0,
+             "collective_ms_median": 30.0 + i, "algorithmic_GBps_median": 34.1, "kernel_us_per_step_rank0": 4.1,
+             "mode_used": f"stream-ordered+graph+fused+program+tokens-fenced+xccl-rccl/{m}",
+             "host_split_us_per_step": {k: 1.0 for k in "abcdefgh"}, "bus_ids": ["0000:05:00.0"] * 8,
+             "devices_seen": [8] * 8, "rank_devices": list(range(8)), "pipedepth": 128, "wall_s": 9.1}
+        if bad:
+            r["error"] = f"mode {m}: rc 1: hiccl_signal_wait: timeout after 60 s on flag 0x7f00 " + "e" * 800
+        c5[m] = r
+    if failing == 7:  # the last mode killed at its limit: the leg stops there
+        c5["stream_graph_fused"]["rc"] = 124
+        c5["stopped_after"] = "stream_graph_fused"
+    c5["protocol_ab"] = bench.c5_protocol_ab(c5)
+    line = {"metric": bench.METRIC, "value": 52000.0, "unit": "GB/s", "n_gpus": 8, "steps": 20, "warmup": 5,
+            "ms_per_step": 1.48, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic", "config": {"workload": "C2 ..." + "c" * 150, "n_inputs": 8},
+            "roofline": {"bound": "hbm", "achieved": 6530.0, "peak": 8000.0, "unit": "GB/s", "frac": 0.816,
+                         "traffic": 9.66e9, "serial_rw_model": {"frac": 0.98, "frac_write_probe": 0.95},
+                         "traffic_from_profile": {"file": "profiles/r06_pmc.json", "box_kernel_ms": 1.45,
+                                                  "fits_this_run": True, "over_algorithmic": 1.00024}},
+            "cpu_baseline": None, "parity_full": None, "parity_sample_ok": True,
+            "device_props": {"gcn_arch": "gfx950:sramecc+:xnack-", "cus": 256}, "control_plane": "gloo", "c5": c5}
+    out = bench.compact_line(line)
+    text = json.dumps(out)
+    assert len(text) < DRIVER_TAIL_CHARS, len(text)
+    back = json.loads(text)["c5"]
+    for i, m in enumerate(C5_MODES):
+        assert back[m]["kat"] == c5[m]["kat"] and back[m]["rc"] == c5[m]["rc"], m
+        assert back[m]["mode_used"] == c5[m]["mode_used"], m
+        if "error" in c5[m]:
+            assert back[m]["error"].startswith(f"mode {m}: rc 1: hiccl_signal_wait"), m
+    assert back.get("stopped_after") == c5.get("stopped_after")
+    ab = back["protocol_ab"]
+    assert ab["baseline_ms"] == 32.0
+    for k in ("stream_graph_fused_fenced", "stream_graph_fused"):
+        assert k in ab
+
+
+def test_traffic_profile_cited_fits_the_run(tmp_path, monkeypatch):
+    """bench.traffic_from_profiles cites the newest PMC profile of the
+    headline kernel whose rocprofv3 kernel time is at or below this run's
+    kernel mean, and says when none fits (VERDICT r05 weak #3)."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    (tmp_path / "profiles").mkdir()
+    for tag, ns in (("r05b", 1444913.0), ("r05n", 1508727.0), ("r02x_misaligned", 1400000.0)):
+        d = {"tag": tag, "n_inputs": 8, "count": 1 << 28, "hbm_bytes_per_launch": 9.666e9,
+             "traffic_over_algorithmic": 1.00024, "rocprof_avg_kernel_ns": ns,
+             "kernel": "void k_reduce_single<OpF32, 256, 4, 11, 0>(SingleArgs)"}
+        if "misaligned" in tag:
+            d["variant"] = "misaligned"
+        (tmp_path / "profiles" / f"{tag}_pmc.json").write_text(json.dumps(d))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    p = bench.traffic_from_profiles(8, 1 << 28, run_kernel_ms=1.4744)
+    assert p["tag"] == "r05b" and p["fits_this_run"] is True and p["profiles_considered"] == 2
+    p = bench.traffic_from_profiles(8, 1 << 28, run_kernel_ms=1.52)
+    assert p["tag"] == "r05n" and p["fits_this_run"] is True
+    p = bench.traffic_from_profiles(8, 1 << 28, run_kernel_ms=1.40)
+    assert p["tag"] == "r05n" and p["fits_this_run"] is False
+    assert bench.traffic_from_profiles(4, 1 << 28, run_kernel_ms=1.5) is None

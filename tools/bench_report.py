@@ -14,7 +14,12 @@ def compact_line(line):
     srw = r.pop("serial_rw_model", None) or {}
     r["serial_rw_frac"] = srw.get("frac_write_probe")
     r["serial_rw_frac_copy_write"] = srw.get("frac")
-    r["traffic_profile"] = (r.pop("traffic_from_profile", None) or {}).get("file")
+    tp = r.pop("traffic_from_profile", None) or {}
+    # the cited profile, its kernel time and whether that time fits this run's
+    # kernel mean (a profile from a slower box does not)
+    r["traffic_profile"] = ({"file": tp.get("file"), "kernel_ms": tp.get("box_kernel_ms"),
+                             "fits_this_run": tp.get("fits_this_run"), "x_alg": tp.get("over_algorithmic")}
+                            if tp else None)
     r.pop("traffic_source", None)
     out["roofline"] = r
     cpu = line.get("cpu_baseline")
@@ -40,6 +45,8 @@ def compact_line(line):
     mis = line.get("c2_misaligned")
     if mis:
         out["c2_misaligned"] = {"shifted_over_aligned": mis.get("shifted_over_aligned"),
+                                "shifted_over_headline": mis.get("shifted_over_headline"),
+                                "aligned_over_headline": mis.get("aligned_over_headline"),
                                 "shifted_frac": mis.get("shifted_frac"),
                                 "parity_ok": all((mis.get("parity_sample_ok") or {"": False}).values())}
     if line.get("c5") is not None:
@@ -50,16 +57,18 @@ def compact_line(line):
 def compact_c5(c5):
     """Per config-5 mode: its known-answer verdict, exit code, median
     collective time and rate, step-kernel time and the mode that ran."""
-    out = {k: c5[k] for k in ("skipped", "workload", "stopped_after", "forced_stream_ordered") if k in c5}
+    out = {k: c5[k] for k in ("skipped", "stopped_after", "forced_stream_ordered") if k in c5}
+    if "workload" in c5:
+        out["workload"] = str(c5["workload"])[:120]
     for name, r in c5.items():
         if not isinstance(r, dict) or name in ("env_scrubbed", "protocol_ab"):
             continue
         m = {"kat": r.get("kat"), "rc": r.get("rc"), "ms": r.get("collective_ms_median"),
              "GBps": r.get("algorithmic_GBps_median"), "kernel_us_step": r.get("kernel_us_per_step_rank0"),
              "mode_used": r.get("mode_used")}
-        for k in ("skipped", "error"):
+        for k in ("skipped", "error"):  # the head of the message names the failure
             if k in r:
-                m[k] = str(r[k])[:160]
+                m[k] = str(r[k])[:100]
         out[name] = {k: v for k, v in m.items() if v is not None}
     ab = c5.get("protocol_ab")
     if ab:
