@@ -77,3 +77,18 @@ def test_second_failure_gets_its_own_suffix(tmp_path):
     assert (out / "r99y_a1_gputest.log").read_text() == "fail1\n"
     assert (out / "r99y_a2_gputest.log").read_text() == "fail2\n"
     assert not (out / "r99y_gputest.log").exists()
+
+
+def test_archive_stays_off_the_gpu_box():
+    """tools/archive/ (retired probes; their results live in profiles/) is
+    not pushed to the GPU box, and nothing the GPU tier, smoke() or bench.py
+    runs imports from it."""
+    import re
+    ignore = open(os.path.join(ROOT, ".gpurunignore")).read().split()
+    assert "./tools/archive" in ignore
+    users = [os.path.join(ROOT, f) for f in ("bench.py", "__graft_entry__.py")]
+    users += [os.path.join(ROOT, "tools", f) for f in os.listdir(os.path.join(ROOT, "tools")) if f.endswith(".py")]
+    users += [os.path.join(ROOT, "tests", f) for f in os.listdir(os.path.join(ROOT, "tests")) if f.endswith(".py")]
+    pat = re.compile(r"^\s*(import|from)\s+\S*archive|sys\.path\.\w+\(.*archive", re.M)
+    for f in users:
+        assert not pat.search(open(f).read()), f

@@ -186,12 +186,19 @@ def roundtrip(args):
     legs = [("serial", serial), ("pipelined", pipelined)]
     expect = host_sum(host_in)
     legs += [(k, (lambda p=p: p.reduce(host_out, host_in))) for k, p in pipes.items()]
+    # the store form each leg's reduction launches take (hiccl_reduce_auto_choice_ex:
+    # write-through by size up to 256 MiB written per launch, else nt)
+    launch_count = {"serial": count, "pipelined": csz,
+                    **{k: p_mib << 20 >> 2 for k, p_mib in zip(pipes, (64, 32, 128))}}
+    form = {k: {2: "nt", 4: "write-through"}[hiccl_amd.auto_choice(torch.float32, c, n)["store_policy"]]
+            for k, c in launch_count.items()}
     out = {}
     for name, fn in legs:
         host_out.zero_()
         wall, _ = B.time_launches(fn, 5, 2)
         t = wall / 5
-        out[name] = {"s": round(t, 4), "GBps_alg": round((n + 1) * count * 4 / t / 1e9, 2)}
+        out[name] = {"s": round(t, 4), "GBps_alg": round((n + 1) * count * 4 / t / 1e9, 2),
+                     "elements_per_launch": launch_count[name], "store_form": form[name]}
         if name.startswith("host_pipe"):
             out[name]["parity_ok"] = bool(torch.equal(host_out.view(torch.int32), expect.view(torch.int32)))
     for p in pipes.values():
