@@ -65,7 +65,7 @@ class ReduceConfig(ctypes.Structure):
                 ("blocks_per_cu", ctypes.c_int), ("nontemporal", ctypes.c_int),
                 ("acc", ctypes.c_int), ("grid", ctypes.c_int), ("store_policy", ctypes.c_int),
                 ("engine", ctypes.c_int), ("schedule", ctypes.c_int), ("grab", ctypes.c_int),
-                ("drain", ctypes.c_int)]
+                ("drain", ctypes.c_int), ("order", ctypes.c_int)]
 
 
 _lib = None

@@ -296,7 +296,7 @@ struct SingleArgs {
   uint32_t n;         // inputs
   uint32_t head;      // scalar elements before the body
   uint32_t tail;      // scalar elements after the body
-  uint32_t pad;
+  uint32_t order;     // log2 of the tile-order segments (0: linear; tile_order)
   uint32_t *sched;    // dynamic unit counter {ticket, done}, or NULL: static grid-stride
   uint32_t grab;      // units per ticket (dynamic schedule), >= 1
   uint32_t drain;     // 1: wait for a unit's stores before the next unit's loads
@@ -566,6 +566,26 @@ __device__ __forceinline__ void for_each_unit(uint32_t *sched, uint32_t grab, ui
   }
 }
 
+// Tile order: unit t of a launch of n units runs tile tile_order(t).  With
+// 2^L segments the order interleaves them -- consecutive units (the ones in
+// flight together across the chip) spread over 2^L equal stretches of every
+// input instead of one contiguous window -- a bijection on [0, n) for any n
+// (segment s holds q + (s < r) tiles, q = n >> L, r = n mod 2^L; the last r
+// units are the long segments' extra tiles).  L = 0: linear.
+__device__ __forceinline__ uint64_t tile_order(uint64_t t, uint64_t n, uint32_t L) {
+  if (!L) return t;
+  const uint64_t S = 1ull << L, q = n >> L, r = n & (S - 1);
+  uint64_t seg, idx;
+  if (t < (q << L)) {
+    seg = t & (S - 1);
+    idx = t >> L;
+  } else {
+    seg = t - (q << L);
+    idx = q;
+  }
+  return seg * q + (seg < r ? seg : r) + idx;
+}
+
 // ------------------------------------------------------------ kernels ------
 
 template <class Op, int BLOCK, int U, int POL, int ENG>
@@ -581,7 +601,8 @@ __global__ __launch_bounds__(BLOCK) void k_reduce_single(SingleArgs a) {
   Shifted<ArgInputs> in{raw, shift};
   char *outb = a.out + shift;
   constexpr uint64_t TILE = (uint64_t)BLOCK * U;
-  for_each_unit(a.sched, a.grab, 0, a.ntiles, [&](uint64_t t, auto hook) {
+  for_each_unit(a.sched, a.grab, 0, a.ntiles, [&](uint64_t u, auto hook) {
+    const uint64_t t = tile_order(u, a.ntiles, a.order);
     const uint64_t pkt0 = t * TILE;
     const uint64_t left = a.npkt - pkt0;
     const uint32_t tile_bytes = (uint32_t)((left < TILE ? left : TILE) * kPacket);
@@ -1226,12 +1247,13 @@ struct Cfg {
   bool store_auto;  // store_policy 0: the store form follows the launch's size (wt_cap)
   bool wt;          // the launch stores write-through by size: decided BEFORE the engine
                     // (oneshot_cfg, plan_cfg), since AUTO's engine rules differ under it
+  int order;        // tile-order segments (hiccl_reduce_config_t.order; 0/1 linear)
 };
 
 // Raw config: zero block/unroll stay zero until the engine is known.
 Cfg resolve(const hiccl_reduce_config_t *c) {
   Cfg r{0, 0, 0, kDefPol % 10, HICCL_ACC_NATIVE, 0, kDefPol / 10, HICCL_ENGINE_AUTO, HICCL_SCHED_AUTO, 0, 0, true,
-        false};
+        false, 0};
   if (c) {
     r.block = c->block;
     r.unroll = c->unroll;
@@ -1245,6 +1267,7 @@ Cfg resolve(const hiccl_reduce_config_t *c) {
     r.schedule = c->schedule;
     r.grab = c->grab;
     r.drain = c->drain;
+    r.order = c->order;
   }
   return r;
 }
@@ -1552,6 +1575,7 @@ std::string plan_shape_error(const Cfg &c, int dtype) {
     return "plan kernels load nt (nontemporal 2) and store nt (store_policy 2), system-scope write-through "
            "(store_policy 4) or either by the launch's size (store_policy 0)";
   if (c.drain) return "plan kernels do not support drain";
+  if (c.order != 0 && c.order != 1) return "plan kernels run their units in linear order (order 0)";
   if (c.engine == HICCL_ENGINE_PHASE) {
     if (c.block != kPhBlock || c.unroll != phase_p_dtype(dtype, c.acc))
       return "plan kernels run the PHASE engine in its default shape only (block 512, unroll " +
@@ -1605,7 +1629,18 @@ int check_cfg_fields(const Cfg &c, const std::string &who) {
   if (c.schedule < HICCL_SCHED_AUTO || c.schedule > HICCL_SCHED_DYNAMIC)
     return fail(hipErrorInvalidValue, who + ": bad schedule");
   if (c.grab < 0 || c.grab > 4096) return fail(hipErrorInvalidValue, who + ": bad grab");
+  if (c.order < 0 || c.order > 4096 || (c.order & (c.order - 1)))
+    return fail(hipErrorInvalidValue, who + ": order must be 0 or a power of two <= 4096");
   return 0;
+}
+
+uint32_t log2u(int v) {
+  uint32_t l = 0;
+  while (v > 1) {
+    v >>= 1;
+    l++;
+  }
+  return l;
 }
 
 uint64_t tiles_for(uint64_t npkt, uint64_t tile) {
@@ -1684,6 +1719,7 @@ int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t c
   if (grid > a.ntiles) grid = a.ntiles;
   a.grab = c.grab > 0 ? (uint32_t)c.grab : default_grab(c.engine, n, c.unroll);
   a.drain = (uint32_t)c.drain;
+  a.order = log2u(c.order);
   a.sched = unit_sched_for(c.engine, n, a.ntiles, grid, dev, s, c.schedule, a.grab, c.unroll);
   fn(a, dim3((unsigned)grid), s);
   return check_hip(hipGetLastError(), "hiccl_reduce: launch");

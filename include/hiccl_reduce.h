@@ -151,6 +151,9 @@ typedef struct {
   int grab;          /* dynamic schedule: units per ticket (0 = default: PHASE 1,
                         TILE ceil(9 / (n + 1))) */
   int drain;         /* 1: a workgroup waits for a unit's stores before the next unit's loads */
+  int order;         /* one-shot calls (n <= 64): units run interleaved over `order` equal
+                        stretches of the bucket (a power of two <= 4096; 0 / 1: linear);
+                        plans: 0 only */
 } hiccl_reduce_config_t;
 
 int hiccl_reduce_ex(int dtype, void *out, const void *const *in, int n, size_t count,

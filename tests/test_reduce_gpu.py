@@ -280,7 +280,10 @@ def test_python_reduce_argument_checks():
     dict(block=256, unroll=4, nontemporal=1, store_policy=3, grid=192),
     dict(block=512, unroll=4, nontemporal=2, store_policy=2, blocks_per_cu=2),
     dict(block=256, unroll=1, grid=7), dict(block=256, unroll=8), dict(block=256, unroll=16),
-    dict(block=256, unroll=8, schedule=2, grab=1, grid=3), dict(block=256, unroll=16, grid=5)])
+    dict(block=256, unroll=8, schedule=2, grab=1, grid=3), dict(block=256, unroll=16, grid=5),
+    # tile order interleaved over 2^L stretches (a bijection for any tile count; static and dynamic)
+    dict(order=2), dict(order=8, grid=3), dict(order=64, schedule=2, grab=1, grid=5), dict(order=4096, unroll=1),
+    dict(order=16, engine=2)])
 def test_tuning_variants_same_bits(oracle, config):
     for n, count in ((8, 1 << 20), (3, 123457)):
         x = oracle.fill(n, count, seed=n)
@@ -1021,7 +1024,7 @@ def test_oneshot_write_through_needs_its_shape():
 
 
 def test_plan_config_refuses_unsupported_fields():
-    for bad in (dict(engine=1, unroll=32), dict(engine=1, unroll=3), dict(engine=2, unroll=4), dict(engine=1, block=512),
+    for bad in (dict(order=2), dict(order=-1), dict(engine=1, unroll=32), dict(engine=1, unroll=3), dict(engine=2, unroll=4), dict(engine=1, block=512),
                 dict(nontemporal=1), dict(store_policy=3), dict(store_policy=1), dict(drain=1), dict(schedule=7),
                 # write-through has no TILE unroll 1 / 8 / 16 plan kernel (refused here, not at launch)
                 dict(store_policy=4, engine=1, unroll=8), dict(store_policy=4, engine=1, unroll=16),
