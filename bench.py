@@ -292,15 +292,22 @@ def whole_job_gbps(world, bytes_per_step, steps, wall_max_s):
 
 # ----------------------------------------------------------- workloads -----
 
-def make_bucket(n, count, dtype=torch.float32, seed=SEED):
+def make_bucket(n, count, dtype=torch.float32, seed=SEED, layout="bucket"):
+    """n inputs (generator-filled) and an output.  layout "bucket": the
+    library's layout, one allocation (hiccl_amd.bucket / hiccl_bucket_alloc);
+    "separate": one torch allocation per buffer."""
     # integer buckets (size_t: the reference drivers' T) get the float
     # generator's bits
     fill_as = {torch.int64: torch.float64, torch.int32: torch.float32}.get(dtype, dtype)
-    ins = [torch.empty(count, dtype=fill_as, device="cuda") for _ in range(n)]
+    if layout == "bucket":
+        ins, out = hiccl_amd.bucket(n, count, fill_as)
+    else:
+        ins = [torch.empty(count, dtype=fill_as, device="cuda") for _ in range(n)]
+        out = torch.empty(count, dtype=fill_as, device="cuda")
     for k, t in enumerate(ins):
         hiccl_amd.fill_uniform(t, seed, k)
     ins = [t.view(dtype) for t in ins]
-    out = torch.empty(count, dtype=dtype, device="cuda")
+    out = out.view(dtype)
     torch.cuda.synchronize()
     return ins, out
 
@@ -738,6 +745,8 @@ def main():
     copy_gbps = copy_ceiling() if dist.rank == 0 else None
     misaligned = (c2_misaligned(n, count, args.steps, args.warmup, headline_s=kern_s)
                   if dist.rank == 0 and cfg is None and not args.no_misaligned else None)
+    layout_ab = (c2_layout_ab(n, count, args.steps, args.warmup, headline_s=kern_s)
+                 if dist.rank == 0 and cfg is None and not args.no_misaligned else None)
     prof = traffic_from_profiles(n, count, run_kernel_ms=kern_s * 1e3) if cfg is None else None
     cpu, parity_full = None, None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
@@ -772,6 +781,9 @@ def main():
         "data": "synthetic (uniform [-1,1) counter-hash, device-generated)",
         "config": {"workload": f"C2: {n} inputs x 2^{args.log2count} fp32 ({count * 4 >> 20} MiB/input) -> 1 output, "
                                "device-resident, one hiccl_reduce launch per step",
+                   "layout": "one bucket allocation (hiccl_bucket_alloc layout: buffer j at j x "
+                             f"{int(L.lib().hiccl_bucket_stride(L.HICCL_FLOAT32, count))} B); separate "
+                             "allocations in c2_layout_ab",
                    "n_inputs": n, "count": count, "bytes_per_step": bytes_step,
                    "kernel_config": cfg or "default", "parallelism": f"replicas x{dist.world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -818,6 +830,8 @@ def main():
     }
     if misaligned is not None:
         line["c2_misaligned"] = misaligned
+    if layout_ab is not None:
+        line["c2_layout_ab"] = layout_ab
     if c5 is not None:
         line["c5"] = c5
     # the full record on stderr, the driver's one line (compact: the driver
@@ -840,12 +854,14 @@ def c2_misaligned(n, count, steps, warmup, headline_s=None):
     the headline (BENCH_r05: 1.5918 vs 1.4744 ms), so the absolute shifted
     rate is `shifted_frac` and `shifted_over_headline` (VERDICT r05 weak #5)."""
     offs = [1 + k % 3 for k in range(n)]
-    bases = [torch.empty(count + 4, dtype=torch.float32, device="cuda") for _ in range(n)]
+    # the headline's layout (one bucket allocation), each input 4 elements
+    # longer for the shifted view
+    bases, out = hiccl_amd.bucket(n, count + 4)
+    out = out[:count]
     for k, b in enumerate(bases):  # element j of base k = generator(k, j), shifted views included
         hiccl_amd.fill_uniform(b, SEED, k)
     aligned = [b[:count] for b in bases]
     shifted = [b[o:o + count] for b, o in zip(bases, offs)]
-    out = torch.empty(count, dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
     runs = {"aligned": lambda: hiccl_amd.reduce(out, aligned), "shifted": lambda: hiccl_amd.reduce(out, shifted)}
@@ -882,6 +898,47 @@ def c2_misaligned(n, count, steps, warmup, headline_s=None):
         res["aligned_over_headline"] = round(t["aligned"] / headline_s, 4)
         res["shifted_over_headline"] = round(t["shifted"] / headline_s, 4)
     del bases, aligned, shifted, out
+    torch.cuda.empty_cache()
+    return res
+
+
+def c2_layout_ab(n, count, steps, warmup, headline_s=None):
+    """The bucket layout against separate allocations, as an interleaved A/B
+    in one process: the headline's layout (one allocation, hiccl_amd.bucket)
+    and the same buffers as n + 1 separate torch allocations (the layout
+    rounds 1-5 measured), launches alternating; outputs compared bit for
+    bit.  Separate allocations leave the streams' relative physical
+    placement to chance: up to 8 % apart between buckets of one process
+    (profiles/r06d_alloc.jsonl)."""
+    legs = {"bucket": make_bucket(n, count), "separate": make_bucket(n, count, layout="separate")}
+    runs = {k: (lambda i=i, o=o: hiccl_amd.reduce(o, i)) for k, (i, o) in legs.items()}
+    for _ in range(warmup):
+        for fn in runs.values():
+            fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    ms = {k: [] for k in runs}
+    for _ in range(steps):
+        for k, fn in runs.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            fn()
+            b.record(s)
+            ms[k].append((a, b))
+    torch.cuda.synchronize()
+    t = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) * 1e-3 for k, v in ms.items()}
+    same = bool(torch.equal(legs["bucket"][1].view(torch.int32), legs["separate"][1].view(torch.int32)))
+    bytes_step = (n + 1) * count * 4
+    res = {"ab": "interleaved launches, one bucket allocation vs n + 1 separate allocations",
+           "bucket_stride_bytes": int(L.lib().hiccl_bucket_stride(L.HICCL_FLOAT32, count)),
+           "bucket_kernel_ms_mean": round(t["bucket"] * 1e3, 4), "separate_kernel_ms_mean": round(t["separate"] * 1e3, 4),
+           "separate_over_bucket": round(t["separate"] / t["bucket"], 4),
+           "bucket_frac": round(bytes_step / t["bucket"] / 1e9 / HBM_PEAK_GBPS, 4),
+           "separate_frac": round(bytes_step / t["separate"] / 1e9 / HBM_PEAK_GBPS, 4),
+           "outputs_identical": same}
+    if headline_s:
+        res["separate_over_headline"] = round(t["separate"] / headline_s, 4)
+    del legs, runs
     torch.cuda.empty_cache()
     return res
 

@@ -109,6 +109,9 @@ _SIGS = {
                                           ctypes.c_uint32, ctypes.c_size_t, _vp]),
     "hiccl_stream_copy": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
     "hiccl_device_info": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp]),
+    "hiccl_bucket_stride": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_size_t]),
+    "hiccl_bucket_alloc": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, _vp, _vp, _vp]),
+    "hiccl_bucket_free": (ctypes.c_int, [_vp]),
     "hiccl_signal_wait": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_uint32, _vp,
                                          ctypes.c_double, _vp]),
     "hiccl_signal_wait_dev": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_uint32, _vp, _vp,

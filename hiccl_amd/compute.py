@@ -96,6 +96,25 @@ def reduce_ptrs(dtype_code, out_ptr, in_ptrs, count, stream=None, config=None):
     L.check(rc, "hiccl_reduce")
 
 
+def bucket(n, count, dtype=torch.float32, device=None):
+    """A reduction bucket in the library's layout (hiccl_bucket_alloc): n
+    inputs and one output of ``count`` elements carved from ONE device
+    allocation, buffer j at j x hiccl_bucket_stride (the buffer rounded up to
+    64 KiB, plus 64 KiB), so the n + 1 streams keep one fixed relative
+    placement.  The slab comes from torch's allocator
+    (one hipMalloc for a fresh large block) and lives as long as any view.
+    Returns (inputs, output): contiguous 1-D views."""
+    esz = torch.empty((), dtype=dtype).element_size()
+    stride = L.lib().hiccl_bucket_stride(L.DTYPE_OF_TORCH.get(dtype, -1), count)
+    if not stride:
+        raise ValueError(f"hiccl: no bucket layout for dtype {dtype}, count {count}")
+    assert stride % esz == 0
+    se = stride // esz
+    slab = torch.empty((n + 1) * se, dtype=dtype, device=device if device is not None else "cuda")
+    views = [slab[j * se:j * se + count] for j in range(n + 1)]
+    return views[:n], views[n]
+
+
 def auto_choice(dtype, count, n, config=None, cus=256):
     """What a one-shot call (and a one-compute plan at TILE unroll 2 / 4 or
     AUTO) resolves to on a GPU of ``cus`` CUs, without a device:

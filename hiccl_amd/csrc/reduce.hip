@@ -2792,4 +2792,51 @@ int hiccl_stream_copy(void *dst, const void *src, size_t bytes, void *stream) {
   return check_hip(hipGetLastError(), "stream_copy: launch");
 }
 
+// ---- bucket layout
+//
+// A reduction bucket -- n inputs and the output of one compute -- in ONE
+// device allocation, buffer j (inputs 0..n-1, then the output) at
+// j x stride, stride = the buffer rounded up to 64 KiB plus 64 KiB.  Measured
+// on config 2 (tools/alloc_probe.py; profiles/r06d_alloc.jsonl,
+// r06e_alloc.jsonl, r06f_alloc.jsonl): the same kernel on nine separate
+// hipMalloc'd buffers (torch.empty, hipMalloc, hipDeviceMallocContiguous)
+// runs 1.43-1.56 ms depending on the allocation -- up to 8 % apart in one
+// process, although every buffer alone reads and writes at the same rate --
+// while buckets laid out in one allocation at 1 GiB + 0-4 MiB strides ran
+// 1.424-1.450 ms, every instance (the 64-128 KiB staggers fastest).  The
+// separate allocations leave the streams' relative physical placement to
+// chance; one allocation fixes it.
+static uint64_t bucket_stride(size_t bytes) {
+  const uint64_t g = 64ull << 10;
+  return (((uint64_t)bytes + g - 1) / g) * g + g;
+}
+
+size_t hiccl_bucket_stride(int dtype, size_t count) {
+  const size_t esz = esize(dtype);
+  return esz && count ? (size_t)bucket_stride(count * esz) : 0;
+}
+
+int hiccl_bucket_alloc(int dtype, int n, size_t count, int device, void **base, void **in, void **out) {
+  const size_t esz = esize(dtype);
+  if (!esz) return fail(hipErrorInvalidValue, "bucket_alloc: unknown dtype");
+  if (n < 0 || n > (1 << 20)) return fail(hipErrorInvalidValue, "bucket_alloc: n out of range");
+  if (!count) return fail(hipErrorInvalidValue, "bucket_alloc: count must be > 0");
+  if (!base || !out || (n > 0 && !in)) return fail(hipErrorInvalidValue, "bucket_alloc: NULL output argument");
+  *base = nullptr;
+  if (int e = check_hip(hipSetDevice(device), "bucket_alloc: hipSetDevice")) return e;
+  const uint64_t stride = bucket_stride(count * esz);
+  char *b = nullptr;
+  if (int e = check_hip(hipMalloc((void **)&b, (size_t)(stride * (uint64_t)(n + 1))), "bucket_alloc: hipMalloc"))
+    return e;
+  for (int k = 0; k < n; k++) in[k] = b + (uint64_t)k * stride;
+  *out = b + (uint64_t)n * stride;
+  *base = b;
+  return 0;
+}
+
+int hiccl_bucket_free(void *base) {
+  if (!base) return 0;
+  return check_hip(hipFree(base), "bucket_free: hipFree");
+}
+
 }  // extern "C"

@@ -444,6 +444,25 @@ int hiccl_stream_copy(void *dst, const void *src, size_t bytes, void *stream);
  * clock (kHz) and memory bus width (bits); NULL outputs are skipped. */
 int hiccl_device_info(int device, int *cus, int *mem_clock_khz, int *bus_width_bits);
 
+/* ----------------------------------------------------------------------
+ * Bucket layout.  A reduction bucket -- n inputs and the output of one
+ * compute, `count` elements each -- in ONE device allocation: buffer j
+ * (inputs 0..n-1, then the output) at base + j * hiccl_bucket_stride(dtype,
+ * count), the buffer's bytes rounded up to 64 KiB plus 64 KiB.  Separate
+ * allocations leave the relative physical placement of the n + 1 streams to
+ * chance, and config 2's kernel time moves by up to 8 % with it; buckets in
+ * one allocation run at the fast end, every instance.
+ * The reduction reads and writes exactly the same bytes either way.
+ *   stride   bytes between consecutive buffers (0 for an unknown dtype or
+ *            count 0).
+ *   alloc    hipMalloc on `device` of (n + 1) strides; in[k] (a host array
+ *            of n pointers) and *out receive the buffers, *base the
+ *            allocation to pass to hiccl_bucket_free.
+ */
+size_t hiccl_bucket_stride(int dtype, size_t count);
+int hiccl_bucket_alloc(int dtype, int n, size_t count, int device, void **base, void **in, void **out);
+int hiccl_bucket_free(void *base);
+
 #ifdef __cplusplus
 }
 #endif

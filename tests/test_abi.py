@@ -251,3 +251,25 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
         L.lib()
     with pytest.raises(ImportError, match="HIP extension missing"):
         hiccl_amd.Compute(torch.float32, device=0)
+
+
+def test_bucket_layout_on_host():
+    """hiccl_bucket_stride: the buffer rounded up to 64 KiB plus 64 KiB
+    (config 2: 1 GiB + 64 KiB); hiccl_bucket_alloc refuses bad arguments
+    before any HIP call."""
+    lib = L.lib()
+    K = 64 << 10
+    assert lib.hiccl_bucket_stride(L.HICCL_FLOAT32, 1 << 28) == (1 << 30) + K
+    assert lib.hiccl_bucket_stride(L.HICCL_FLOAT32, 1) == 2 * K
+    assert lib.hiccl_bucket_stride(L.HICCL_BFLOAT16, K // 2) == 2 * K
+    assert lib.hiccl_bucket_stride(L.HICCL_BFLOAT16, K // 2 + 1) == 3 * K
+    assert lib.hiccl_bucket_stride(99, 10) == 0 and lib.hiccl_bucket_stride(L.HICCL_FLOAT32, 0) == 0
+    base, out = ctypes.c_void_p(), ctypes.c_void_p()
+    ins = (ctypes.c_void_p * 8)()
+    for args, word in (((99, 8, 16, 0), "dtype"), ((0, -1, 16, 0), "n out of range"), ((0, 8, 0, 0), "count"),
+                       ((0, 8, 16, 0, None, ins, ctypes.byref(out)), "NULL"),
+                       ((0, 8, 16, 0, ctypes.byref(base), None, ctypes.byref(out)), "NULL")):
+        full = args if len(args) == 7 else args + (ctypes.byref(base), ins, ctypes.byref(out))
+        assert lib.hiccl_bucket_alloc(*full) == 1
+        assert word in L.last_error()
+    assert lib.hiccl_bucket_free(None) == 0

@@ -394,10 +394,16 @@ def test_driver_line_stays_compact():
             "device_props": {"gcn_arch": "gfx950", "cus": 256, "mem_clock_khz": 2000000},
             "c2_misaligned": {"shifted_over_aligned": 1.007, "shifted_frac": 0.78, "shifted_over_headline": 1.09,
                               "aligned_over_headline": 1.08,
-                              "parity_sample_ok": {"aligned": True, "shifted": True}}, "c5": c5}
+                              "parity_sample_ok": {"aligned": True, "shifted": True}},
+            "c2_layout_ab": {"ab": "x" * 80, "bucket_stride_bytes": 1073807360, "bucket_kernel_ms_mean": 1.44,
+                             "separate_kernel_ms_mean": 1.52, "separate_over_bucket": 1.0556,
+                             "separate_over_headline": 1.05, "bucket_frac": 0.839, "separate_frac": 0.795,
+                             "outputs_identical": True}, "c5": c5}
     out = bench.compact_line(line)
     text = json.dumps(out)
     assert len(text) < 3500, len(text)
+    assert out["c2_layout_ab"] == {"separate_over_bucket": 1.0556, "separate_over_headline": 1.05, "bucket_frac": 0.839,
+                                   "separate_frac": 0.795, "outputs_identical": True}
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config"):
         assert out[k] == line[k]
@@ -427,7 +433,9 @@ def test_compact_c5_skipped_leg():
 
 C5_MODES = ("host", "stream_graph", "stream_graph_fused_noprog", "stream_graph_fused_fenced",
             "flat_stream_graph_fused", "xccl", "stream_graph_fused")
-DRIVER_TAIL_CHARS = 3500  # the compact line's budget: BENCH_r04's whole stdout tail was 3,166 chars
+# the compact line's budget: BENCH_r05's stdout_tail held 7,344 characters
+# (the 2.9 KB line, then stderr); the worst-case N = 8 line stays near half
+DRIVER_TAIL_CHARS = 4000
 
 
 @pytest.mark.parametrize("failing", [0, 3, 7])
@@ -464,7 +472,12 @@ def test_driver_line_keeps_every_c5_mode_at_n8(failing):
                          "traffic_from_profile": {"file": "profiles/r06_pmc.json", "box_kernel_ms": 1.45,
                                                   "fits_this_run": True, "over_algorithmic": 1.00024}},
             "cpu_baseline": None, "parity_full": None, "parity_sample_ok": True,
-            "device_props": {"gcn_arch": "gfx950:sramecc+:xnack-", "cus": 256}, "control_plane": "gloo", "c5": c5}
+            "device_props": {"gcn_arch": "gfx950:sramecc+:xnack-", "cus": 256}, "control_plane": "gloo",
+            "c2_misaligned": {"shifted_over_aligned": 1.0093, "shifted_frac": 0.7519, "shifted_over_headline": 1.0903,
+                              "aligned_over_headline": 1.0796, "parity_sample_ok": {"aligned": True, "shifted": True}},
+            "c2_layout_ab": {"separate_over_bucket": 1.0556, "separate_over_headline": 1.05, "bucket_frac": 0.839,
+                             "separate_frac": 0.795, "outputs_identical": True},
+            "c5": c5}
     out = bench.compact_line(line)
     text = json.dumps(out)
     assert len(text) < DRIVER_TAIL_CHARS, len(text)

@@ -8,6 +8,8 @@ misaligned inputs (partition() element offsets), in-place outputs, bf16 in
 both accumulation modes, size_t known-answer, the batched plan vs the
 reference's one-launch-per-compute structure, and a full-size sampled check.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -1153,3 +1155,44 @@ def test_misaligned_full_tiles(oracle, offs, out_off, dtype):
         got = gpu_reduce(x, count, dtype, offsets=offs, out_offset=out_off, config=cfg)
         exp = oracle.reduce(list(x), dtype=dtype)
         assert bits_equal(got, exp), f"offs={offs} out={out_off} count={count}: {first_mismatch(got, exp)}"
+
+
+def test_bucket_layout_alloc_and_reduce(oracle):
+    """hiccl_bucket_alloc (C ABI) and hiccl_amd.bucket (Python): n inputs and
+    the output in one allocation at hiccl_bucket_stride; the reduction over
+    them gives the oracle's bits (the layout only moves where the bytes
+    live)."""
+    lib = hiccl_amd.lib()
+    n, count = 8, (1 << 20) + 5
+    stride = lib.hiccl_bucket_stride(L.HICCL_FLOAT32, count)
+    base, out = ctypes.c_void_p(), ctypes.c_void_p()
+    ins = (ctypes.c_void_p * n)()
+    L.check(lib.hiccl_bucket_alloc(L.HICCL_FLOAT32, n, count, 0, ctypes.byref(base), ins, ctypes.byref(out)),
+            "bucket_alloc")
+    try:
+        assert [ins[k] - base.value for k in range(n)] == [k * stride for k in range(n)]
+        assert out.value - base.value == n * stride
+        x = oracle.fill(n, count, seed=606)
+        for k in range(n):
+            t = torch.from_numpy(x[k]).to(DEV)
+            L.check(lib.hiccl_stream_copy(ctypes.c_void_p(ins[k]), ctypes.c_void_p(t.data_ptr()), count * 4, None),
+                    "copy")
+        torch.cuda.synchronize()
+        hiccl_amd.reduce_ptrs(L.HICCL_FLOAT32, out.value, [ins[k] for k in range(n)], count)
+        got = torch.empty(count, device=DEV)
+        L.check(lib.hiccl_stream_copy(ctypes.c_void_p(got.data_ptr()), out, count * 4, None), "copy")
+        torch.cuda.synchronize()
+        assert bits_equal(got.cpu().numpy(), oracle.reduce(list(x)))
+    finally:
+        L.check(lib.hiccl_bucket_free(base), "bucket_free")
+    # the Python views: same layout, bf16 too
+    for dt, npdt in ((torch.float32, np.float32), (torch.bfloat16, np.uint16)):
+        vi, vo = hiccl_amd.bucket(5, count, dt)
+        st = lib.hiccl_bucket_stride(L.DTYPE_OF_TORCH[dt], count)
+        assert [v.data_ptr() - vi[0].data_ptr() for v in vi + [vo]] == [j * st for j in range(6)]
+        x = oracle.fill(5, count, seed=707, dtype=npdt)
+        for k in range(5):
+            vi[k].copy_(to_dev(x[k]))
+        hiccl_amd.reduce(vo, vi)
+        torch.cuda.synchronize()
+        assert bits_equal(to_host(vo, npdt), oracle.reduce(list(x), dtype=npdt))

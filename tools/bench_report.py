@@ -49,6 +49,10 @@ def compact_line(line):
                                 "aligned_over_headline": mis.get("aligned_over_headline"),
                                 "shifted_frac": mis.get("shifted_frac"),
                                 "parity_ok": all((mis.get("parity_sample_ok") or {"": False}).values())}
+    lab = line.get("c2_layout_ab")
+    if lab:
+        out["c2_layout_ab"] = {k: lab.get(k) for k in ("separate_over_bucket", "separate_over_headline", "bucket_frac",
+                                                       "separate_frac", "outputs_identical")}
     if line.get("c5") is not None:
         out["c5"] = compact_c5(line["c5"])
     return out
