@@ -1753,6 +1753,8 @@ int hiccl_reduce_auto_choice_ex(int dtype, const hiccl_reduce_config_t *cfg, siz
   // the same refusals as hiccl_reduce_ex: a shape no kernel has is an error
   const bool has = n > kMaxArgInputs ? plan_shape_error(c, dtype).empty() : pick_single_dtype(dtype, c) != nullptr;
   if (!has) return fail(hipErrorInvalidValue, "auto_choice: no kernel for this config and dtype");
+  if (c.bpc < 1 || c.bpc > 64) return fail(hipErrorInvalidValue, "auto_choice: blocks_per_cu");
+  if (c.grid < 0) return fail(hipErrorInvalidValue, "auto_choice: grid < 0");
   const uint64_t units = tiles_for(npkt, (uint64_t)c.block * c.unroll);  // tiles or phased chunks
   const uint64_t grid = std::min<uint64_t>(c.grid > 0 ? (uint64_t)c.grid : (uint64_t)cus * c.bpc, units);
   const bool dyn = wants_dynamic(c.engine, n, units, grid, c.schedule, (uint32_t)c.grab, c.unroll);
@@ -2823,11 +2825,14 @@ int hiccl_bucket_alloc(int dtype, int n, size_t count, int device, void **base, 
   if (!count) return fail(hipErrorInvalidValue, "bucket_alloc: count must be > 0");
   if (!base || !out || (n > 0 && !in)) return fail(hipErrorInvalidValue, "bucket_alloc: NULL output argument");
   *base = nullptr;
+  int prev = 0;
+  if (int e = check_hip(hipGetDevice(&prev), "bucket_alloc: hipGetDevice")) return e;
   if (int e = check_hip(hipSetDevice(device), "bucket_alloc: hipSetDevice")) return e;
   const uint64_t stride = bucket_stride(count * esz);
   char *b = nullptr;
-  if (int e = check_hip(hipMalloc((void **)&b, (size_t)(stride * (uint64_t)(n + 1))), "bucket_alloc: hipMalloc"))
-    return e;
+  const int e = check_hip(hipMalloc((void **)&b, (size_t)(stride * (uint64_t)(n + 1))), "bucket_alloc: hipMalloc");
+  (void)hipSetDevice(prev);  // the caller's current device is left as it was
+  if (e) return e;
   for (int k = 0; k < n; k++) in[k] = b + (uint64_t)k * stride;
   *out = b + (uint64_t)n * stride;
   *base = b;

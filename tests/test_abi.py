@@ -212,7 +212,8 @@ def test_auto_choice_ex_store_form_and_refusals():
     for cfg, n in ((dict(store_policy=4, engine=T, unroll=8), 2), (dict(store_policy=4, engine=T, unroll=8), 65),
                    (dict(store_policy=4, engine=T, unroll=1), 65), (dict(block=512, unroll=4), 70),
                    (dict(engine=7), 2), (dict(acc=5), 2), (dict(schedule=9), 2),
-                   (dict(order=3), 2), (dict(order=8192), 2), (dict(order=-2), 2), (dict(order=2), 65)):
+                   (dict(order=3), 2), (dict(order=8192), 2), (dict(order=-2), 2), (dict(order=2), 65),
+                   (dict(blocks_per_cu=65), 2), (dict(grid=-1), 2)):
         with pytest.raises(hiccl_amd.HicclError):
             hiccl_amd.auto_choice(f32, 1 << 16, n, config=cfg)
     # n > 64 with unroll 8 and nt: the plan kernel has it
