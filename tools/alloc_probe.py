@@ -52,13 +52,15 @@ class Bucket:
             self.keep = ts
             ptrs = [t.data_ptr() for t in ts]
         elif form.startswith("pool"):
-            # pool[+<extra KiB>][:desc][:outfirst]: one allocation, buffer j at
-            # j x (1 GiB + extra); desc: inputs in descending order; outfirst:
-            # the output at slot 0
+            # pool[c][+<extra KiB>][:desc][:outfirst]: one allocation, buffer j
+            # at j x (1 GiB + extra); poolc: hipDeviceMallocContiguous; desc:
+            # inputs in descending order; outfirst: the output at slot 0
             spec = form.split(":")
-            extra = int(spec[0][5:]) * 1024 if spec[0].startswith("pool+") else 0
+            contig = spec[0].startswith("poolc")
+            head = spec[0][5:] if contig else spec[0][4:]
+            extra = int(head[1:]) * 1024 if head.startswith("+") else 0
             stride = BYTES + extra
-            base = hip_alloc((N + 1) * stride)
+            base = hip_alloc((N + 1) * stride, CONTIGUOUS if contig else None)
             self.raw = [base]
             slots = list(range(N + 1))
             if "outfirst" in spec:
@@ -115,18 +117,40 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--forms", default="torch,hipmalloc,contig,pool")
+    ap.add_argument("--fragment", type=int, default=0, help="seed: fragment free device memory before allocating")
+    ap.add_argument("--interleave", action="store_true", help="forms in round-robin allocation order")
     args = ap.parse_args()
     probe = ctypes.CDLL(os.path.join(ROOT, "tools", "libhbm_probe.so"))
     probe.probe_run.restype = ctypes.c_int
     probe.probe_run.argtypes = [ctypes.c_int] * 7 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                                      ctypes.c_uint64, ctypes.c_void_p]
+    frag = []
+    if args.fragment:
+        # fragment the device's free memory first: allocate ~2/3 of it in
+        # pieces of 96 MiB-1.5 GiB, free every other one (kept until the end)
+        rng = np.random.default_rng(args.fragment)
+        free_b, _ = torch.cuda.mem_get_info()
+        total, pieces = 0, []
+        while total < free_b * 2 // 3:
+            nb = int(rng.integers(96, 1536)) << 20
+            pieces.append(hip_alloc(nb))
+            total += nb
+        for k, p in enumerate(pieces):
+            if k % 2:
+                HIP.hipFree(ctypes.c_void_p(p))
+            else:
+                frag.append(p)
+        print(json.dumps({"fragmented": True, "pieces": len(pieces), "held_GiB": round(total / 2 / 2**30, 1)}),
+              flush=True)
     buckets = []
-    for form in args.forms.split(","):
-        for _ in range(args.buckets):
-            try:
-                buckets.append(Bucket(form))
-            except MemoryError as e:
-                print(json.dumps({"form": form, "error": str(e)}), flush=True)
+    forms = args.forms.split(",")
+    order = ([f for _ in range(args.buckets) for f in forms] if args.interleave
+             else [f for f in forms for _ in range(args.buckets)])
+    for form in order:
+        try:
+            buckets.append(Bucket(form))
+        except MemoryError as e:
+            print(json.dumps({"form": form, "error": str(e)}), flush=True)
     torch.cuda.synchronize()
     ref = torch.empty(COUNT, device="cuda")
     hiccl_amd.reduce_ptrs(L.HICCL_FLOAT32, ref.data_ptr(), buckets[0].ins, COUNT)
@@ -161,6 +185,8 @@ def main():
     print(json.dumps({"summary": summ}), flush=True)
     for bk in buckets:
         bk.free()
+    for p in frag:
+        HIP.hipFree(ctypes.c_void_p(p))
     return 0
 
 
