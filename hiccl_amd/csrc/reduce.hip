@@ -2799,15 +2799,17 @@ int hiccl_stream_copy(void *dst, const void *src, size_t bytes, void *stream) {
 // A reduction bucket -- n inputs and the output of one compute -- in ONE
 // device allocation, buffer j (inputs 0..n-1, then the output) at
 // j x stride, stride = the buffer rounded up to 64 KiB plus 64 KiB.  Measured
-// on config 2 (tools/alloc_probe.py; profiles/r06d_alloc.jsonl,
-// r06e_alloc.jsonl, r06f_alloc.jsonl): the same kernel on nine separate
-// hipMalloc'd buffers (torch.empty, hipMalloc, hipDeviceMallocContiguous)
-// runs 1.43-1.56 ms depending on the allocation -- up to 8 % apart in one
-// process, although every buffer alone reads and writes at the same rate --
-// while buckets laid out in one allocation at 1 GiB + 0-4 MiB strides ran
-// 1.424-1.450 ms, every instance (the 64-128 KiB staggers fastest).  The
-// separate allocations leave the streams' relative physical placement to
-// chance; one allocation fixes it.
+// on config 2 (tools/alloc_probe.py; profiles/r06d_alloc.jsonl, r06e_, r06f_,
+// r06h_): the same kernel on nine separate hipMalloc'd buffers (torch.empty,
+// hipMalloc, hipDeviceMallocContiguous) runs 1.43-1.56 ms depending on the
+// allocation -- up to 9 % apart in one process, although every buffer alone
+// reads and writes at the same rate -- while buckets in one allocation at
+// 1 GiB + 0-4 MiB strides ran 1.424-1.462 ms, every one of 28 instances on
+// fresh devices (the 64-128 KiB staggers fastest).  Separate allocations
+// leave the streams' relative physical placement to chance; one allocation
+// fixes it.  Which physical memory the allocation gets still matters: on a
+// device whose free memory was fragmented first, later buckets can be as
+// slow as separate buffers (r06l_alloc.jsonl).
 static uint64_t bucket_stride(size_t bytes) {
   const uint64_t g = 64ull << 10;
   return (((uint64_t)bytes + g - 1) / g) * g + g;
