@@ -26,7 +26,7 @@ sys.path.insert(0, ROOT)
 import hiccl_amd  # noqa: E402
 from hiccl_amd import _lib as L  # noqa: E402
 
-N, COUNT, SEED = 8, 1 << 28, 1234
+N, COUNT, SEED = 8, 1 << 28, 1234  # --n / --log2count override
 BYTES = COUNT * 4
 HIP = ctypes.CDLL("libamdhip64.so.7")
 HIP.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
@@ -60,6 +60,8 @@ class Bucket:
             head = spec[0][5:] if contig else spec[0][4:]
             extra = int(head[1:]) * 1024 if head.startswith("+") else 0
             stride = BYTES + extra
+            if head.startswith("x"):  # poolx<k>: stride k/2 x the buffer + 64 KiB
+                stride = int(head[1:]) * BYTES // 2 + (64 << 10)
             base = hip_alloc((N + 1) * stride, CONTIGUOUS if contig else None)
             self.raw = [base]
             slots = list(range(N + 1))
@@ -119,7 +121,12 @@ def main():
     ap.add_argument("--forms", default="torch,hipmalloc,contig,pool")
     ap.add_argument("--fragment", type=int, default=0, help="seed: fragment free device memory before allocating")
     ap.add_argument("--interleave", action="store_true", help="forms in round-robin allocation order")
+    ap.add_argument("--n", type=int, default=8)
+    ap.add_argument("--log2count", type=int, default=28)
     args = ap.parse_args()
+    global N, COUNT, BYTES
+    N, COUNT = args.n, 1 << args.log2count
+    BYTES = COUNT * 4
     probe = ctypes.CDLL(os.path.join(ROOT, "tools", "libhbm_probe.so"))
     probe.probe_run.restype = ctypes.c_int
     probe.probe_run.argtypes = [ctypes.c_int] * 7 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
@@ -172,7 +179,7 @@ def main():
         del out
         r = {"bucket": i, "form": bk.form, "kernel_ms_mean": round(float(np.mean(ms[i])), 4),
              "kernel_ms_min": round(float(np.min(ms[i])), 4),
-             "frac_of_8TBs": round(9 * BYTES / (np.mean(ms[i]) * 1e-3) / 8e12, 4),
+             "frac_of_8TBs": round((N + 1) * BYTES / (np.mean(ms[i]) * 1e-3) / 8e12, 4),
              "buffer_GBps_read_inputs_then_write_output": buffer_rates(bk, probe, 5), "bit_exact": ok,
              "addresses_GiB": [round(p / 2**30, 3) for p in bk.ins + [bk.out]]}
         res.append(r)
