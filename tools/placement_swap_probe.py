@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--buckets", type=int, default=6)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--engines", action="store_true",
+                    help="also every bucket under the phased engine and the static tile schedule")
     args = ap.parse_args()
     buckets = []
     for _ in range(args.buckets):
@@ -65,6 +67,11 @@ def main():
     t = mean_ms({b: (lambda b=b: hiccl_amd.reduce(buckets[b][1], buckets[b][0])) for b in range(len(buckets))},
                 args.reps, args.rounds)
     print(json.dumps({"buckets_ms": t}), flush=True)
+    if args.engines:
+        cfgs = {"phase": dict(engine=2), "tile_static": dict(engine=1, unroll=4, schedule=1)}
+        fns = {f"{b}:{k}": (lambda b=b, c=c: hiccl_amd.reduce(buckets[b][1], buckets[b][0], config=c))
+               for b in range(len(buckets)) for k, c in cfgs.items()}
+        print(json.dumps({"buckets_engines_ms": mean_ms(fns, args.reps, args.rounds)}), flush=True)
     s = max(t, key=t.get)
     f = min(t, key=t.get)
     (si, so), (fi, fo) = buckets[s], buckets[f]
