@@ -41,6 +41,11 @@ int main(int argc, char **argv) {
   CHECK(hiccl_host_pipe_create(&pipe, 99, 0, 0, 0) != 0 && pipe == NULL);
   hiccl_reduce_plan_destroy(NULL);
   hiccl_host_pipe_destroy(NULL);
+  /* bucket layout: the stride rule and the host-side refusals */
+  CHECK(hiccl_bucket_stride(HICCL_FLOAT32, (size_t)1 << 28) == ((size_t)1 << 30) + 65536);
+  CHECK(hiccl_bucket_stride(99, 16) == 0);
+  CHECK(hiccl_bucket_alloc(HICCL_FLOAT32, 2, 16, 0, NULL, NULL, NULL) != 0 && strstr(hiccl_last_error(), "NULL"));
+  CHECK(hiccl_bucket_free(NULL) == 0);
   if (argc > 1 && strcmp(argv[1], "gpu") == 0) {
     enum { N = 3, COUNT = 1000 };
     float host[N][COUNT], out[COUNT];
@@ -69,6 +74,18 @@ int main(int argc, char **argv) {
     }
     for (k = 0; k < N; k++) hipFree(dev[k]);
     hipFree(dout);
+    { /* the same sum in a bucket (hiccl_bucket_alloc): same bits */
+      void *base = NULL, *bin[N], *bout = NULL;
+      float out2[COUNT];
+      CHECK(hiccl_bucket_alloc(HICCL_FLOAT32, N, COUNT, 0, &base, bin, &bout) == 0);
+      CHECK((char *)bin[1] - (char *)bin[0] == (ptrdiff_t)hiccl_bucket_stride(HICCL_FLOAT32, COUNT));
+      for (k = 0; k < N; k++) CHECK(hipMemcpy(bin[k], host[k], sizeof(host[k]), 1) == 0);
+      CHECK(hiccl_reduce(HICCL_FLOAT32, bout, (const void *const *)bin, N, COUNT, NULL) == 0);
+      CHECK(hipDeviceSynchronize() == 0);
+      CHECK(hipMemcpy(out2, bout, sizeof(out2), 2) == 0);
+      CHECK(memcmp(out, out2, sizeof(out)) == 0);
+      CHECK(hiccl_bucket_free(base) == 0);
+    }
   }
   printf("abi_c: %s\n", fails ? "FAILED" : "PASSED");
   return fails ? 1 : 0;

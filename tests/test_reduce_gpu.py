@@ -665,7 +665,8 @@ def test_byte_copy_exact(nbytes):
 def test_plain_c_client_on_gpu():
     """build/abi_c (tests/cpp/abi_c.c, built by make): a C99 program using
     only include/hiccl_reduce.h reduces 3 device buffers, bit-exact with a
-    host loop in the reference's order."""
+    host loop in the reference's order, then the same sum in a bucket from
+    hiccl_bucket_alloc, bit-identical."""
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "abi_c")
