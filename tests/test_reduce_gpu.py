@@ -1197,3 +1197,25 @@ def test_bucket_layout_alloc_and_reduce(oracle):
         hiccl_amd.reduce(vo, vi)
         torch.cuda.synchronize()
         assert bits_equal(to_host(vo, npdt), oracle.reduce(list(x), dtype=npdt))
+
+
+@pytest.mark.parametrize("dtype,n", [(np.float64, 3), (np.float32, 70), (np.int32, 9)], ids=["f64-3", "f32-70", "i32-9"])
+def test_bucket_layout_more_shapes(oracle, dtype, n):
+    """hiccl_amd.bucket for other types and for n > 64 (the plan kernel via
+    the device pointer table), with a ragged count: the oracle's bits."""
+    count = 300007
+    tdt = TORCH_OF[np.dtype(dtype)]
+    if np.dtype(dtype) == np.dtype(np.int32):
+        x = np.random.default_rng(n).integers(-2**31, 2**31, (n, count), dtype=np.int32)
+    else:
+        x = oracle.fill(n, count, seed=900 + n, dtype=dtype)
+    ins, out = hiccl_amd.bucket(n, count, tdt)
+    st = hiccl_amd.lib().hiccl_bucket_stride(L.DTYPE_OF_TORCH[tdt], count)
+    assert ins[1].data_ptr() - ins[0].data_ptr() == st and out.data_ptr() - ins[0].data_ptr() == n * st
+    for k in range(n):
+        ins[k].copy_(to_dev(x[k]).view(tdt))
+    hiccl_amd.reduce(out, ins)
+    torch.cuda.synchronize()
+    e = oracle.reduce(list(x), dtype=dtype)
+    got = to_host(out, dtype)
+    assert bits_equal(got, e), first_mismatch(got, e)
